@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s (pixels x spp / s) of the MI355X path-tracing hot path on walled.yml.
+
+One step = one launch of the megakernel over this rank's pixels for `--spp-per-step` samples
+(the reference's gpu_render_batch, walled.yml: 1000), plus — for N > 1 — the frame-end RCCL
+gather of every rank's tile radiance to rank 0.  Inputs (scene, KD tree) are resident in HBM
+before the timed region.  N GPUs: one process per GPU (torch.distributed.run), image rows
+sharded as 32-row stripes dealt round-robin.  Weak scaling: at N GPUs a step renders N x
+spp-per-step samples for every pixel, so each rank keeps the work of the 1-GPU step
+(W*H/N pixels x N*spp samples) and the image stays bit-identical to the 1-GPU one (the RNG and
+the running mean are keyed on the global pixel and absolute sample index).
+
+Prints ONE JSON line (rank 0) with `roofline` (algorithmic bytes of the trace kernel per
+launch / its HIP-event duration vs 8 TB/s HBM) and `cpu_baseline` (the oracle restatement of
+the reference CPU renderer on this host, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+STRIPE = 32
+# Canonical per-event byte sizes of the roofline
+BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits": 32, "mesh_hits": 132}
+
+
+def rank_tiles(width, height, rank, world):
+    tiles = []
+    for i, y0 in enumerate(range(0, height, STRIPE)):
+        if i % world == rank:
+            tiles.append((0, y0, width, min(STRIPE, height - y0)))
+    return tiles
+
+
+def roofline_bytes_per_sample(ctx, width, height, spp=16):
+    """Algorithmic bytes per sample from the device's own work counters on every 16th pixel
+    in x and y, 16 spp."""
+    tiles = [(x, y, 1, 1) for y in range(0, height, 16) for x in range(0, width, 16)]
+    c = ctx.count_work(tiles, 0, spp)
+    total = sum(BYTES[k] * c[k] for k in BYTES)
+    trav = sum(BYTES[k] * c[k] for k in ("nodes", "leaf_refs", "sphere_tests", "tri_tests"))
+    return total / c["samples"], trav / c["samples"], c
+
+
+def cpu_baseline(loaded, target_s=10.0, threads=None):
+    """The oracle (C++ restatement of render_to_target_cpu) on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py  # test infrastructure: the CPU baseline leg only
+
+    threads = threads or min(16, os.cpu_count() or 1)
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    # calibrate on a band of rows, then run a sample sized for ~target_s
+    band = [(0, 0, w, 64)]
+    t0 = time.perf_counter()
+    oracle_py.render(loaded, band, 0, 1, threads=threads)
+    dt = max(time.perf_counter() - t0, 1e-3)
+    rate = w * 64 / dt
+    spp = max(1, min(64, int(target_s * rate / (w * h))))
+    t0 = time.perf_counter()
+    oracle_py.render(loaded, [(0, 0, w, h)], 0, spp, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"full {w}x{h} frame, {spp} spp, oracle/oracle.cpp (recursive radiance), "
+                      f"{threads} threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="walled")
+    ap.add_argument("--spp-per-step", type=int, default=None,
+                    help="samples per pixel per launch (default: the scheme's gpu_render_batch)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from rt_amd import render, scheme
+
+    sch = scheme.load_json(os.path.join(ROOT, "tests", "golden", "scenes", args.scene + ".json"))
+    loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets"))
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    spp = args.spp_per_step or int(sch["render_info"].get("gpu_render_batch") or 1)
+    tiles = rank_tiles(w, h, rank, world)
+    npix = sum(t[2] * t[3] for t in tiles)
+    max_npix = max(sum(t[2] * t[3] for t in rank_tiles(w, h, r, world)) for r in range(world))
+
+    ctx = render.Context(loaded, device=local)
+    out = torch.zeros((max_npix, 4), dtype=torch.float32, device=f"cuda:{local}")
+    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def barrier():
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    sample = 0
+
+    spp_rank = spp * world  # weak scaling: per-rank work is the 1-GPU step's
+
+    def step():
+        nonlocal sample
+        ctx.render_device(out.data_ptr(), tiles, sample, spp_rank)
+        sample += spp_rank
+        if dist:
+            dist.gather(out, gather_list=gather, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(ctx.last_kernel_ms())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_samples = w * h * spp_rank * args.steps
+    value = total_samples / elapsed / 1e6
+    res = {"metric": "Msamples/s (pixels x spp / s) on walled.yml" if args.scene == "walled"
+           else f"Msamples/s (pixels x spp / s) on {args.scene}.yml",
+           "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic-free: the reference's own scene file (tests/golden/scenes), seeded RNG",
+           "config": {"workload": f"{args.scene}.yml {w}x{h}, {spp} spp x n_gpus per step (one launch per rank), "
+                                  f"kd_tree_depth {int(loaded.info.kd_tree_depth)}",
+                      "spp_per_step": spp, "pixels": w * h, "stripes": f"{STRIPE}-row round-robin",
+                      "parallelism": f"tiles{world}"}}
+
+    if rank == 0 and not args.no_roofline:
+        bps, trav_bps, counts = roofline_bytes_per_sample(ctx, w, h)
+        avg_ms = sum(kernel_ms) / len(kernel_ms)
+        achieved = bps * npix * spp_rank / (avg_ms * 1e-3) / 1e9
+        res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                           "kernel": "trace_kernel<false>", "kernel_ms_avg": round(avg_ms, 3),
+                           "bytes_per_sample": round(bps, 1), "traversal_bytes_per_sample": round(trav_bps, 1),
+                           "samples_per_launch": npix * spp_rank,
+                           "counts_per_sample": {k: round(v / counts["samples"], 3) for k, v in counts.items()
+                                                 if k != "samples"}}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(loaded, args.cpu_seconds)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

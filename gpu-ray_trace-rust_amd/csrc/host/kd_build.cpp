@@ -1,0 +1,235 @@
+// kd_build.cpp — host side of the boundary: KD-tree build + flattening, camera conversion,
+// RGBA8 conversion.  Compiled with -ffp-contract=off so every f32 rounding step equals the
+// reference's (Rust never contracts a*b+c).
+//
+// rt_kd_build restates KdTree::build / node_from_elems (src/accel/kdtree.rs:26-56,107-137)
+// iteratively and writes the 8-byte node layout of rt_abi.h directly, breadth first, so the
+// top L levels of the tree are a prefix of the node array (the device stages that prefix in
+// LDS).  The split of a node is the f32 sequential mean of its elements' AABB centroids on
+// the node's axis (Sum<Vector3<f32>> folds from zero in element order, kdtree.rs:113); an
+// element goes high when aabb.high >= split and low when aabb.low <= split (both allowed,
+// kdtree.rs:119-127); a node is a leaf when depth > max_depth or it holds <= 1 element.
+#include "host_internal.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <vector>
+
+namespace rth {
+
+static inline float rmin(float a, float b) { return std::fmin(a, b); }  // Rust f32::min
+static inline float rmax(float a, float b) { return std::fmax(a, b); }  // Rust f32::max
+
+int gather_renderables(const rt_scene_desc* sc, std::vector<Renderable>* out) {
+    if (!sc) return RT_ERR_INVALID_ARG;
+    out->clear();
+    for (uint32_t i = 0; i < sc->n_elems; ++i) {
+        const rt_elem& e = sc->elems[i];
+        Renderable r{};
+        r.kind = e.kind;
+        r.index = e.index;
+        switch (e.kind) {
+            case RT_ELEM_SPHERE: {  // Sphere::give_aabb (sphere.rs:106-114)
+                if (e.index >= sc->n_spheres) return RT_ERR_INVALID_ARG;
+                const rt_sphere& s = sc->spheres[e.index];
+                r.has_aabb = true;
+                for (int a = 0; a < 3; ++a) { r.lo[a] = s.c[a] - s.r; r.hi[a] = s.c[a] + s.r; }
+                break;
+            }
+            case RT_ELEM_FREE_TRI: {  // Triangle::give_aabb (generic.rs:138-156)
+                if (e.index >= sc->n_free_tris) return RT_ERR_INVALID_ARG;
+                const rt_free_triangle& t = sc->free_tris[e.index];
+                r.has_aabb = true;
+                for (int a = 0; a < 3; ++a) {
+                    r.lo[a] = rmin(rmin(t.verts[0][a], t.verts[1][a]), t.verts[2][a]);
+                    r.hi[a] = rmax(rmax(t.verts[0][a], t.verts[1][a]), t.verts[2][a]);
+                }
+                break;
+            }
+            case RT_ELEM_CUBE_MAP:  // DistantCubeMap::give_aabb -> None
+                if (e.index >= sc->n_cube_maps) return RT_ERR_INVALID_ARG;
+                r.has_aabb = false;
+                break;
+            default:
+                return RT_ERR_INVALID_ARG;
+        }
+        out->push_back(r);
+    }
+    uint32_t mesh_tri = 0;
+    for (uint32_t m = 0; m < sc->n_meshes; ++m) {
+        const rt_mesh& mesh = sc->meshes[m];
+        for (uint32_t p = 0; p < mesh.n_prims; ++p) {
+            const rt_mesh_prim& pr = mesh.prims[p];
+            for (uint32_t t = 0; t < pr.n_tris; ++t) {
+                Renderable r{};
+                r.kind = RT_KIND_MESH_TRI;
+                r.index = mesh_tri++;
+                r.has_aabb = true;
+                for (int a = 0; a < 3; ++a) {
+                    float v0 = pr.poses[3 * (size_t)pr.indices[3 * (size_t)t + 0] + a];
+                    float v1 = pr.poses[3 * (size_t)pr.indices[3 * (size_t)t + 1] + a];
+                    float v2 = pr.poses[3 * (size_t)pr.indices[3 * (size_t)t + 2] + a];
+                    r.lo[a] = rmin(rmin(v0, v1), v2);
+                    r.hi[a] = rmax(rmax(v0, v1), v2);
+                }
+                out->push_back(r);
+            }
+        }
+    }
+    return RT_OK;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+struct KdTreeOwned {
+    rt_kd_tree pub;
+    std::vector<rt_kd_node> nodes;
+    std::vector<uint32_t> refs;
+    std::vector<uint32_t> uncond;
+};
+
+extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd_tree** out) {
+    if (!scene || !out) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    std::vector<Renderable> rs;
+    int st = gather_renderables(scene, &rs);
+    if (st) return st;
+    KdTreeOwned* kt = new (std::nothrow) KdTreeOwned();
+    if (!kt) return RT_ERR_OOM;
+    std::memset(&kt->pub, 0, sizeof(kt->pub));
+
+    // elems_and_aabbs / unconditional split (draw_scene.rs:60-68)
+    std::vector<uint32_t> root;
+    for (uint32_t i = 0; i < rs.size(); ++i) {
+        if (rs[i].has_aabb) root.push_back(i);
+        else kt->uncond.push_back(i);
+    }
+    uint32_t max_leaf_depth = 0;
+    if (!root.empty()) {
+        // root Aabb: per-axis reduce with f32::min / f32::max (kdtree.rs:29-49)
+        for (int a = 0; a < 3; ++a) {
+            float lo = rs[root[0]].lo[a], hi = rs[root[0]].hi[a];
+            for (size_t k = 1; k < root.size(); ++k) {
+                lo = rmin(lo, rs[root[k]].lo[a]);
+                hi = rmax(hi, rs[root[k]].hi[a]);
+            }
+            kt->pub.bounds[2 * a] = lo;
+            kt->pub.bounds[2 * a + 1] = hi;
+        }
+        struct Item { uint32_t node; uint32_t depth; std::vector<uint32_t> elems; };
+        std::deque<Item> q;
+        kt->nodes.push_back(rt_kd_node{0, 0});
+        q.push_back(Item{0, 0, std::move(root)});
+        while (!q.empty()) {
+            Item it = std::move(q.front());
+            q.pop_front();
+            const uint32_t axis = it.depth % 3;
+            if (it.depth > max_depth || it.elems.size() <= 1) {
+                if (kt->refs.size() + it.elems.size() >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
+                kt->nodes[it.node].a = (uint32_t)it.elems.size();
+                kt->nodes[it.node].b = ((uint32_t)kt->refs.size() << 2) | RT_KD_LEAF;
+                kt->refs.insert(kt->refs.end(), it.elems.begin(), it.elems.end());
+                if (it.depth > max_leaf_depth) max_leaf_depth = it.depth;
+                continue;
+            }
+            float sum = 0.0f;  // centroid component on `axis`, folded in element order
+            for (uint32_t e : it.elems) sum = sum + 0.5f * (rs[e].lo[axis] + rs[e].hi[axis]);
+            const float split = sum / (float)it.elems.size();
+            std::vector<uint32_t> low, high;
+            for (uint32_t e : it.elems) {
+                if (rs[e].hi[axis] >= split) high.push_back(e);
+                if (rs[e].lo[axis] <= split) low.push_back(e);
+            }
+            const uint32_t child = (uint32_t)kt->nodes.size();
+            if (child + 2 >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
+            std::memcpy(&kt->nodes[it.node].a, &split, 4);
+            kt->nodes[it.node].b = (child << 2) | axis;
+            kt->nodes.push_back(rt_kd_node{0, 0});
+            kt->nodes.push_back(rt_kd_node{0, 0});
+            std::vector<uint32_t>().swap(it.elems);
+            q.push_back(Item{child, it.depth + 1, std::move(low)});
+            q.push_back(Item{child + 1, it.depth + 1, std::move(high)});
+        }
+    }
+    kt->pub.n_nodes = (uint32_t)kt->nodes.size();
+    kt->pub.n_refs = (uint32_t)kt->refs.size();
+    kt->pub.max_leaf_depth = max_leaf_depth;
+    kt->pub.n_unconditional = (uint32_t)kt->uncond.size();
+    kt->pub.nodes = kt->nodes.data();
+    kt->pub.refs = kt->refs.data();
+    kt->pub.unconditional = kt->uncond.data();
+    *out = &kt->pub;
+    return RT_OK;
+}
+
+extern "C" void rt_kd_free(rt_kd_tree* tree) {
+    if (!tree) return;
+    // pub is the first member of KdTreeOwned
+    delete reinterpret_cast<KdTreeOwned*>(tree);
+}
+
+// From<pr::Cam> for scene::Cam (src/builder/pr/cam.rs:19-81) after apply_corrections
+// (src/builder/mod.rs:69-72).  Rotation3::from_euler_angles(roll, pitch, yaw) = Rz(yaw)
+// Ry(pitch) Rx(roll) in nalgebra's row-major constructor order; R*v via gemv column order.
+extern "C" int rt_camera_from_scheme(const float d[3], const float o[3], const float up[3],
+                                     float screen_width, float screen_height, uint32_t has_lens,
+                                     float lens_r, const float view_eulers[3], rt_camera* out) {
+    if (!d || !o || !up || !view_eulers || !out) return RT_ERR_INVALID_ARG;
+    float n = std::sqrt((up[0] * up[0] + up[1] * up[1]) + up[2] * up[2]);
+    float u[3] = {up[0] / n, up[1] / n, up[2] / n};
+    float sr = std::sin(view_eulers[0]), cr = std::cos(view_eulers[0]);
+    float sp = std::sin(view_eulers[1]), cp = std::cos(view_eulers[1]);
+    float sy = std::sin(view_eulers[2]), cy = std::cos(view_eulers[2]);
+    float R[3][3] = {
+        {cy * cp, cy * sp * sr - sy * cr, cy * sp * cr + sy * sr},
+        {sy * cp, sy * sp * sr + cy * cr, sy * sp * cr - cy * sr},
+        {-sp, cp * sr, cp * cr},
+    };
+    for (int i = 0; i < 3; ++i) {
+        out->d[i] = (R[i][0] * d[0] + R[i][1] * d[1]) + R[i][2] * d[2];
+        out->up[i] = (R[i][0] * u[0] + R[i][1] * u[1]) + R[i][2] * u[2];
+        out->o[i] = o[i];
+    }
+    out->screen_width = screen_width;
+    out->screen_height = screen_height;
+    out->has_lens = has_lens ? 1u : 0u;
+    out->lens_r = lens_r;
+    return RT_OK;
+}
+
+// rgb_f_to_u8 (draw_scene.rs:104-108): (f.clamp(0,1) * 255 + 0.5).trunc() as u8; `as u8`
+// saturates and maps NaN to 0; alpha 255 (draw_scene.rs:93).
+extern "C" int rt_rgba_to_u8(const float* rgba, uint64_t n_pixels, uint8_t* out) {
+    if ((!rgba || !out) && n_pixels) return RT_ERR_INVALID_ARG;
+    for (uint64_t p = 0; p < n_pixels; ++p) {
+        for (int c = 0; c < 3; ++c) {
+            float f = rgba[4 * p + c];
+            if (f < 0.0f) f = 0.0f;
+            if (f > 1.0f) f = 1.0f;
+            float g = std::trunc(f * 255.0f + 0.5f);
+            out[4 * p + c] = std::isnan(g) ? 0 : (g >= 255.0f ? 255 : (uint8_t)g);
+        }
+        out[4 * p + 3] = 255;
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+extern "C" const char* rt_status_string(int s) {
+    switch (s) {
+        case RT_OK: return "ok";
+        case RT_ERR_INVALID_ARG: return "invalid argument";
+        case RT_ERR_OOM: return "out of memory";
+        case RT_ERR_HIP: return "HIP runtime error";
+        case RT_ERR_UNSUPPORTED: return "unsupported on the device path";
+        case RT_ERR_NO_DEVICE: return "no such gfx950 device";
+        case RT_ERR_BATCH: return "samps_per_pix is not divisible by gpu_render_batch";
+        default: return "unknown status";
+    }
+}

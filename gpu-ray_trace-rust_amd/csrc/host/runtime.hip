@@ -1,0 +1,410 @@
+// runtime.hip — host runtime behind the C ABI: device pick, scene flattening and upload,
+// launches, events, errors.  Replaces GPUState / ComputePipeline
+// (src/render/gpu_utils.rs:257-724) and the batch loop of render_to_target_gpu
+// (src/render/draw_scene.rs:17-47).  Host float work here (RayCompute) is compiled with
+// -ffp-contract=off, like the oracle.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../../include/rt_abi.h"
+#include "../kernel/device_scene.h"
+#include "host_internal.h"
+
+using namespace rtd;
+using namespace rth;
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    DevScene sc{};
+    std::vector<void*> allocs;
+    float4* accum = nullptr;
+    DevTile* d_tiles = nullptr;
+    uint32_t d_tiles_cap = 0;
+    float4* d_out = nullptr;
+    uint64_t d_out_cap = 0;
+    DevCounts* d_counts = nullptr;
+    float last_ms = 0.f;
+    std::string err;
+};
+
+#define HIPCHK(ctx, call)                                                          \
+    do {                                                                           \
+        hipError_t e_ = (call);                                                    \
+        if (e_ != hipSuccess) {                                                    \
+            if (ctx) (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_); \
+            return RT_ERR_HIP;                                                     \
+        }                                                                          \
+    } while (0)
+
+static int set_err(rt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+template <class T>
+static int upload(rt_ctx* c, const std::vector<T>& v, const T** out) {
+    *out = nullptr;
+    if (v.empty()) return RT_OK;
+    void* p = nullptr;
+    if (hipMalloc(&p, v.size() * sizeof(T)) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
+    c->allocs.push_back(p);
+    HIPCHK(c, hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = static_cast<const T*>(p);
+    return RT_OK;
+}
+
+static bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+extern "C" int rt_device_count(int* n) {
+    if (!n) return RT_ERR_INVALID_ARG;
+    *n = 0;
+    int total = 0;
+    if (hipGetDeviceCount(&total) != hipSuccess) return RT_OK;
+    for (int d = 0; d < total; ++d) *n += is_gfx950(d) ? 1 : 0;
+    return RT_OK;
+}
+
+static DevMat make_mat(const rt_material& m, const float rgb[3]) {
+    DevMat d{};
+    for (int i = 0; i < 3; ++i) {
+        d.rgb[i] = rgb[i];
+        d.em[i] = m.has_emissive ? m.emissive[i] : 0.0f;
+    }
+    d.divert = m.divert;
+    d.diffp = m.diffp;
+    d.n_out = m.n_out;
+    d.n_in = m.n_in;
+    return d;
+}
+
+static void destroy_ctx(rt_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipSetDevice(c->device);
+    for (void* p : c->allocs) (void)hipFree(p);
+    if (c->accum) (void)hipFree(c->accum);
+    if (c->d_tiles) (void)hipFree(c->d_tiles);
+    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->d_counts) (void)hipFree(c->d_counts);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* cam,
+                       const rt_render_info* info, const rt_kd_tree* tree_in) {
+    if (info->width == 0 || info->height == 0) return set_err(c, RT_ERR_INVALID_ARG, "empty frame");
+    if ((uint64_t)info->width * info->height >= (1ull << 31))
+        return set_err(c, RT_ERR_INVALID_ARG, "frame too large");
+    if (info->dir_light_samp)
+        return set_err(c, RT_ERR_UNSUPPORTED, "dir_light_samp is not implemented on the device path");
+    if (scene->n_meshes)
+        return set_err(c, RT_ERR_UNSUPPORTED, "mesh triangles are not implemented on the device path yet");
+
+    std::vector<Renderable> rs;
+    int st = gather_renderables(scene, &rs);
+    if (st) return set_err(c, st, "invalid scene description");
+
+    rt_kd_tree* built = nullptr;
+    const rt_kd_tree* tree = tree_in;
+    if (!tree) {
+        st = rt_kd_build(scene, info->kd_tree_depth, &built);
+        if (st) return set_err(c, st, "KD build failed");
+        tree = built;
+    }
+    struct Guard { rt_kd_tree* t; ~Guard() { rt_kd_free(t); } } guard{built};
+
+    if (tree->max_leaf_depth > (uint32_t)MAX_STACK)
+        return set_err(c, RT_ERR_UNSUPPORTED, "KD tree deeper than the device traversal stack");
+    for (uint32_t i = 0; i < tree->n_nodes; ++i) {  // validate topology before any launch
+        const rt_kd_node& n = tree->nodes[i];
+        uint32_t k = n.b >> 2;
+        if ((n.b & 3u) == RT_KD_LEAF) {
+            if ((uint64_t)k + n.a > tree->n_refs) return set_err(c, RT_ERR_INVALID_ARG, "leaf refs out of range");
+        } else if (k + 1 >= tree->n_nodes || k <= i) {
+            return set_err(c, RT_ERR_INVALID_ARG, "KD child index out of range");
+        }
+    }
+
+    // device refs: renderable index -> (kind, index of kind)
+    std::vector<uint32_t> refs(tree->n_refs);
+    for (uint32_t i = 0; i < tree->n_refs; ++i) {
+        uint32_t ri = tree->refs[i];
+        if (ri >= rs.size() || !rs[ri].has_aabb) return set_err(c, RT_ERR_INVALID_ARG, "bad leaf ref");
+        uint32_t kind = rs[ri].kind == RT_KIND_SPHERE ? K_SPHERE : (rs[ri].kind == RT_KIND_FREE_TRI ? K_FREE_TRI : K_MESH_TRI);
+        refs[i] = (kind << REF_KIND_SHIFT) | rs[ri].index;
+    }
+    std::vector<uint2> nodes(tree->n_nodes);
+    for (uint32_t i = 0; i < tree->n_nodes; ++i) nodes[i] = make_uint2(tree->nodes[i].a, tree->nodes[i].b);
+
+    std::vector<float4> sph(scene->n_spheres);
+    std::vector<DevMat> sph_mat(scene->n_spheres);
+    for (uint32_t i = 0; i < scene->n_spheres; ++i) {
+        const rt_sphere& s = scene->spheres[i];
+        sph[i] = make_float4(s.c[0], s.c[1], s.c[2], s.r);
+        sph_mat[i] = make_mat(s.mat, s.rgb);
+    }
+    std::vector<float4> ftri(3 * (size_t)scene->n_free_tris), ftri_n(scene->n_free_tris);
+    std::vector<DevMat> ftri_mat(scene->n_free_tris);
+    for (uint32_t i = 0; i < scene->n_free_tris; ++i) {
+        const rt_free_triangle& t = scene->free_tris[i];
+        for (int k = 0; k < 3; ++k) ftri[3 * i + k] = make_float4(t.verts[k][0], t.verts[k][1], t.verts[k][2], 0.f);
+        ftri_n[i] = make_float4(t.norm[0], t.norm[1], t.norm[2], 0.f);
+        ftri_mat[i] = make_mat(t.mat, t.rgb);
+    }
+
+    DevScene& d = c->sc;
+    std::memset(&d, 0, sizeof(d));
+    std::vector<float> texels;
+    for (uint32_t u = 0; u < tree->n_unconditional; ++u) {
+        const Renderable& r = rs[tree->unconditional[u]];
+        if (r.kind != RT_KIND_CUBE_MAP) continue;
+        const rt_cube_map& cm = scene->cube_maps[r.index];
+        for (int f = 0; f < 6; ++f) {
+            int ti = cm.face[f].texture;
+            if (ti < 0 || (uint32_t)ti >= scene->n_textures) return set_err(c, RT_ERR_INVALID_ARG, "bad cube face texture");
+            const rt_texture& tx = scene->textures[ti];
+            if (!tx.rgb || !tx.width || !tx.height) return set_err(c, RT_ERR_INVALID_ARG, "empty texture");
+            d.face[f].off = (uint32_t)(texels.size() / 3);
+            d.face[f].w = tx.width;
+            d.face[f].h = tx.height;
+            d.face[f].us = cm.face[f].us;
+            d.face[f].vs = cm.face[f].vs;
+            texels.insert(texels.end(), tx.rgb, tx.rgb + 3 * (size_t)tx.width * tx.height);
+        }
+        d.has_cube = 1;
+        break;  // closest_ray_hit over the unconditional list: all hit at +inf, the first wins
+    }
+
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreate(&c->ev0));
+    HIPCHK(c, hipEventCreate(&c->ev1));
+    if ((st = upload(c, nodes, &d.nodes))) return st;
+    if ((st = upload(c, refs, &d.refs))) return st;
+    if ((st = upload(c, sph, &d.sph))) return st;
+    if ((st = upload(c, sph_mat, &d.sph_mat))) return st;
+    if ((st = upload(c, ftri, &d.ftri))) return st;
+    if ((st = upload(c, ftri_n, &d.ftri_n))) return st;
+    if ((st = upload(c, ftri_mat, &d.ftri_mat))) return st;
+    if ((st = upload(c, texels, &d.texels))) return st;
+    d.n_nodes = tree->n_nodes;
+    d.lds_nodes = tree->n_nodes < (uint32_t)LDS_NODES ? tree->n_nodes : (uint32_t)LDS_NODES;
+    for (int i = 0; i < 6; ++i) d.bounds[i] = tree->bounds[i];
+
+    // RayCompute::new (generate.rs:13-23)
+    const int w = (int)info->width, h = (int)info->height;
+    d.x_cf = cam->screen_width / (float)w;
+    d.y_cf = cam->screen_height / (float)h;
+    {
+        float dn = std::sqrt((cam->d[0] * cam->d[0] + cam->d[1] * cam->d[1]) + cam->d[2] * cam->d[2]);
+        float nd[3] = {cam->d[0] / dn, cam->d[1] / dn, cam->d[2] / dn};
+        const float* up = cam->up;
+        float cr[3] = {nd[1] * up[2] - nd[2] * up[1], nd[2] * up[0] - nd[0] * up[2], nd[0] * up[1] - nd[1] * up[0]};
+        float cn = std::sqrt((cr[0] * cr[0] + cr[1] * cr[1]) + cr[2] * cr[2]);
+        for (int i = 0; i < 3; ++i) d.right[i] = cr[i] / cn;
+    }
+    d.x_off = (float)w / 2.0f;
+    d.y_off = (float)h / 2.0f;
+    for (int i = 0; i < 3; ++i) {
+        d.cam_d[i] = cam->d[i];
+        d.cam_o[i] = cam->o[i];
+        d.cam_up[i] = cam->up[i];
+    }
+    d.has_lens = cam->has_lens ? 1u : 0u;
+    d.lens_r = cam->lens_r;
+    d.width = info->width;
+    d.height = info->height;
+    d.assured_depth = info->assured_depth;
+    d.debug_single_ray = info->debug_single_ray ? 1u : 0u;
+    d.seed = info->seed;
+
+    const size_t npix = (size_t)info->width * info->height;
+    if (hipMalloc(&c->accum, npix * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "accumulator alloc failed");
+    HIPCHK(c, hipMemset(c->accum, 0, npix * sizeof(float4)));
+    if (hipMalloc(&c->d_counts, sizeof(DevCounts)) != hipSuccess) return set_err(c, RT_ERR_OOM, "counter alloc failed");
+    return RT_OK;
+}
+
+extern "C" int rt_create(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_info* info,
+                         const rt_kd_tree* tree, int device, rt_ctx** out) {
+    if (!scene || !cam || !info || !out) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int total = 0;
+    if (hipGetDeviceCount(&total) != hipSuccess || device < 0 || device >= total || !is_gfx950(device))
+        return RT_ERR_NO_DEVICE;
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) return RT_ERR_OOM;
+    c->device = device;
+    int st = create_impl(c, scene, cam, info, tree);
+    if (st) {
+        std::fprintf(stderr, "rt_create: %s\n", c->err.c_str());
+        destroy_ctx(c);
+        return st;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+// Builds the per-launch tile table; returns the number of output pixels.
+static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, LaunchArgs* a,
+                         uint64_t* n_out) {
+    if (!tiles || n_tiles == 0) return set_err(c, RT_ERR_INVALID_ARG, "no tiles");
+    std::vector<DevTile> dt(n_tiles);
+    uint64_t blocks = 0, pix = 0;
+    for (uint32_t i = 0; i < n_tiles; ++i) {
+        const rt_tile& t = tiles[i];
+        if (t.w == 0 || t.h == 0 || (uint64_t)t.x0 + t.w > c->sc.width || (uint64_t)t.y0 + t.h > c->sc.height)
+            return set_err(c, RT_ERR_INVALID_ARG, "tile outside the frame");
+        DevTile& d = dt[i];
+        d.x0 = t.x0; d.y0 = t.y0; d.w = t.w; d.h = t.h;
+        d.out_off = (uint32_t)pix;
+        d.block_begin = (uint32_t)blocks;
+        d.bx = (t.w + BLOCK_W - 1) / BLOCK_W;
+        blocks += (uint64_t)d.bx * ((t.h + BLOCK_H - 1) / BLOCK_H);
+        pix += (uint64_t)t.w * t.h;
+    }
+    if (blocks >= (1ull << 31) || pix >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels");
+    if (n_tiles > c->d_tiles_cap) {
+        if (c->d_tiles) (void)hipFree(c->d_tiles);
+        c->d_tiles = nullptr;
+        c->d_tiles_cap = 0;
+        if (hipMalloc(&c->d_tiles, n_tiles * sizeof(DevTile)) != hipSuccess) return set_err(c, RT_ERR_OOM, "tile alloc failed");
+        c->d_tiles_cap = n_tiles;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_tiles, dt.data(), n_tiles * sizeof(DevTile), hipMemcpyHostToDevice, c->stream));
+    a->sc = c->sc;
+    a->tiles = c->d_tiles;
+    a->n_tiles = n_tiles;
+    a->n_blocks = (uint32_t)blocks;
+    a->accum = c->accum;
+    *n_out = pix;
+    return RT_OK;
+}
+
+static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                       uint32_t sample_count, float4* dev_out) {
+    LaunchArgs a{};
+    uint64_t n_out = 0;
+    int st = prepare_tiles(c, tiles, n_tiles, &a, &n_out);
+    if (st) return st;
+    a.sample_begin = sample_begin;
+    a.sample_count = sample_count;
+    a.out = dev_out;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_trace(a, c->stream));  // count 0 still (re)writes the accumulators
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    return RT_OK;
+}
+
+static int ensure_out(rt_ctx* c, uint64_t n) {
+    if (n <= c->d_out_cap) return RT_OK;
+    if (c->d_out) (void)hipFree(c->d_out);
+    c->d_out = nullptr;
+    c->d_out_cap = 0;
+    if (hipMalloc(&c->d_out, n * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "output alloc failed");
+    c->d_out_cap = n;
+    return RT_OK;
+}
+
+static uint64_t tile_pixels(const rt_tile* tiles, uint32_t n) {
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < n; ++i) p += (uint64_t)tiles[i].w * tiles[i].h;
+    return p;
+}
+
+extern "C" int rt_render(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                         uint32_t sample_count, float* out_rgba) {
+    if (!c || !tiles) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t n = tile_pixels(tiles, n_tiles);
+    int st;
+    if (out_rgba && (st = ensure_out(c, n))) return st;
+    if ((st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, out_rgba ? c->d_out : nullptr))) return st;
+    if (out_rgba)
+        HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return RT_OK;
+}
+
+extern "C" int rt_render_device(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles,
+                                uint64_t sample_begin, uint32_t sample_count, float* out_dev) {
+    if (!c || !tiles || !out_dev) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    int st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, reinterpret_cast<float4*>(out_dev));
+    if (st) return st;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    return RT_OK;
+}
+
+extern "C" int rt_last_kernel_ms(const rt_ctx* c, float* ms) {
+    if (!c || !ms) return RT_ERR_INVALID_ARG;
+    *ms = c->last_ms;
+    return RT_OK;
+}
+
+extern "C" int rt_count_work(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                             uint32_t sample_count, rt_work_counts* out) {
+    if (!c || !tiles || !out) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    LaunchArgs a{};
+    uint64_t n_out = 0;
+    int st = prepare_tiles(c, tiles, n_tiles, &a, &n_out);
+    if (st) return st;
+    a.sample_begin = sample_begin;
+    a.sample_count = sample_count;
+    a.counts = c->d_counts;
+    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, sizeof(DevCounts), c->stream));
+    if (sample_count) HIPCHK(c, launch_trace_count(a, c->stream));
+    DevCounts h{};
+    HIPCHK(c, hipMemcpyAsync(&h, c->d_counts, sizeof(DevCounts), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    out->samples = h.samples; out->segments = h.segments; out->nodes = h.nodes;
+    out->leaf_refs = h.leaf_refs; out->sphere_tests = h.sphere_tests; out->tri_tests = h.tri_tests;
+    out->hits = h.hits; out->mesh_hits = h.mesh_hits;
+    return RT_OK;
+}
+
+extern "C" const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int rt_destroy(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    destroy_ctx(c);
+    return RT_OK;
+}
+
+// render_to_target_gpu (draw_scene.rs:17-47) on one device: spp/batch launches over the whole
+// frame; after each, the RGBA8 target is refreshed and the update hook runs.
+extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* cam,
+                                   const rt_render_info* info, uint32_t spp, uint32_t batch, int device,
+                                   uint8_t* target, rt_update_hook hook, void* user) {
+    if (!scene || !cam || !info || !target || batch == 0) return RT_ERR_INVALID_ARG;
+    if (spp % batch != 0) return RT_ERR_BATCH;
+    rt_ctx* c = nullptr;
+    int st = rt_create(scene, cam, info, nullptr, device, &c);
+    if (st) return st;
+    const rt_tile full{0, 0, info->width, info->height};
+    std::vector<float> rgba((size_t)info->width * info->height * 4);
+    for (uint32_t s = 0; s < spp; s += batch) {
+        st = rt_render(c, &full, 1, s, batch, rgba.data());
+        if (st) break;
+        rt_rgba_to_u8(rgba.data(), (uint64_t)info->width * info->height, target);
+        if (hook) hook(user, s + batch);
+    }
+    rt_destroy(c);
+    return st;
+}

@@ -1,0 +1,93 @@
+// device_scene.h — the scene as laid out in HBM for the gfx950 megakernel.
+// Shared by the host runtime (upload) and the kernel (reads).  Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+constexpr int BLOCK = 128;       // threads per workgroup (2 waves): 16 x 8 pixels
+constexpr int BLOCK_W = 16;
+constexpr int BLOCK_H = 8;
+constexpr int MAX_STACK = 24;    // traversal stack entries per thread (>= max_leaf_depth)
+constexpr int LDS_NODES = 2047;  // top of the BFS-ordered node array staged in LDS (16 KiB)
+
+// Device ref encoding: kind in the top 2 bits, index into the kind's arrays below.
+constexpr uint32_t REF_KIND_SHIFT = 30;
+constexpr uint32_t REF_INDEX_MASK = (1u << 30) - 1u;
+enum : uint32_t { K_SPHERE = 0, K_FREE_TRI = 1, K_MESH_TRI = 2 };
+
+// Shading record of a sphere / free triangle (UniformDiffuseSpec + Coloring).  48 bytes.
+struct DevMat {
+    float rgb[3];
+    float em[3];       // zero when the material has no emissive (sphere.rs:70-75)
+    uint32_t divert;   // rt_divert
+    float diffp;
+    float n_out, n_in;
+    uint32_t _pad[2];
+};
+
+struct DevFace {       // one DistantCubeMap face: texel offset, size, uv scales
+    uint32_t off, w, h;
+    float us, vs;
+};
+
+struct DevScene {
+    // KD tree (rt_kd_node layout), breadth-first
+    const uint2* nodes;
+    const uint32_t* refs;   // device-encoded refs
+    uint32_t n_nodes;
+    uint32_t lds_nodes;     // min(n_nodes, LDS_NODES)
+    float bounds[6];
+    // spheres
+    const float4* sph;      // c.xyz, r
+    const DevMat* sph_mat;
+    // free triangles
+    const float4* ftri;     // 3 per triangle: v0, v1, v2 (w unused)
+    const float4* ftri_n;   // uniform normal
+    const DevMat* ftri_mat;
+    // cube map (first unconditional renderable, distant_cube_map.rs); has_cube == 0: misses are black
+    uint32_t has_cube;
+    DevFace face[6];
+    const float* texels;    // f32 RGB pool
+    // camera (RayCompute, generate.rs:13-23, precomputed on host)
+    float cam_d[3], cam_o[3], cam_up[3], right[3];
+    float x_cf, y_cf, x_off, y_off;
+    uint32_t has_lens;
+    float lens_r;
+    uint32_t width, height;
+    int32_t assured_depth;
+    uint32_t debug_single_ray;
+    uint64_t seed;
+};
+
+struct DevTile {
+    uint32_t x0, y0, w, h;
+    uint32_t out_off;       // first output pixel of the tile
+    uint32_t block_begin;   // first workgroup of the tile
+    uint32_t bx;            // workgroups per tile row
+    uint32_t _pad;
+};
+
+struct DevCounts {
+    unsigned long long samples, segments, nodes, leaf_refs, sphere_tests, tri_tests, hits, mesh_hits;
+};
+
+struct LaunchArgs {
+    DevScene sc;
+    const DevTile* tiles;
+    uint32_t n_tiles;
+    uint32_t n_blocks;
+    uint64_t sample_begin;
+    uint32_t sample_count;
+    float4* accum;          // width*height running means
+    float4* out;            // tile-concatenated output (may alias nothing)
+    DevCounts* counts;      // instrumented launch only
+};
+
+// Launch wrappers (trace.hip).
+hipError_t launch_trace(const LaunchArgs& a, hipStream_t s);
+hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s);
+
+}  // namespace rtd

@@ -1,0 +1,441 @@
+// trace.hip — the gfx950 per-pixel path-tracing megakernel.
+//
+// One lane owns one pixel of a tile for the whole sample range of the launch and keeps the
+// pixel's running mean in registers (draw_scene.rs:81-83), so HBM sees one accumulator read
+// and one write per pixel per launch.  Per sample the lane runs the reference CPU path
+// (render_to_target_cpu -> radiance, draw_scene.rs:73-84, radiance.rs:20-72) as a loop:
+// camera ray (generate.rs:24-66) -> KD stack traversal (kdtree.rs:58-104) with the leaf test
+// of closest_hit.rs:6-30 -> hit_info / Russian roulette / continue_ray of the hit element
+// (sphere.rs, triangle/generic.rs, distant_cube_map.rs, material/*.rs).
+//
+// The traversal stack lives in LDS (one column per lane).  A stack entry is (far node, t):
+// the exit distance of a popped entry is the t of the entry below it (or the root exit),
+// which is what kdtree.rs:85-87 pushes, so 8 bytes per entry suffice.
+//
+// Float order matches the oracle operation for operation (compiled with -ffp-contract=off,
+// correctly rounded div/sqrt); the only intended differences are the accumulation order of
+// the bounce estimator (forward L += T*e instead of the reference's recursion) and ocml's
+// sinf/cosf/powf against glibc's — DESIGN.md §Numerics.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/rt_abi.h"
+#include "../../../include/rt_rng.h"
+#include "device_scene.h"
+
+namespace rtd {
+
+constexpr float EPS = 1e-4f;            // src/lib.rs:20
+constexpr float HIT_MIN = EPS * 20.0f;  // closest_hit.rs:16
+constexpr float PI = 3.14159265358979323846f;
+constexpr float RR_THRES = 0.4f;        // radiance.rs:77
+// The reference has no depth cap (radiance.rs:44); past assured_depth a path survives a bounce
+// with p = 0.4, so a cap of 1024 bounces changes an estimate with probability < 0.4^1000.
+// It only guarantees that a corrupted scene cannot hang the GPU.
+constexpr int MAX_BOUNCES = 1024;
+
+struct V3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator-(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 operator*(float s, V3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ V3 operator/(V3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ V3 cmul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ V3 normalize(V3 a) {
+    float n = sqrtf(dot(a, a));
+    return a / n;
+}
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float comp(V3 v, uint32_t a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+__device__ __forceinline__ V3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ V3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
+
+// RayLen ordering (hit.rs:50-76): NaN sorts above everything.
+__device__ __forceinline__ bool raylen_less(float a, float b) {
+    if (__builtin_isnan(a)) return false;
+    if (__builtin_isnan(b)) return true;
+    return a < b;
+}
+
+struct Ray {
+    V3 d, o;
+};
+
+struct Hit {
+    uint32_t ref;   // device ref (kind | index); 0xffffffff = cube map
+    float l;
+    float bu, bv;   // triangle barycentrics
+};
+constexpr uint32_t REF_CUBE = 0xffffffffu;
+
+template <bool COUNT>
+struct Ctr {
+    uint32_t nodes = 0, leaf_refs = 0, sph = 0, tri = 0, segments = 0, hits = 0, mesh_hits = 0;
+};
+
+// ---------------------------------------------------------------- primitives
+// Sphere::intersect (sphere.rs:83-105)
+__device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
+    V3 oc = r.o - xyz(s);
+    float dir = dot(r.d, oc);
+    float consts = dot(oc, oc) - s.w * s.w;
+    float thing2 = dir * dir - consts;
+    if (!(thing2 > 0.0f)) return false;
+    float offset = -dir;
+    float thing = sqrtf(thing2);
+    float l0 = offset + thing, l1 = offset - thing;
+    bool have = false;
+    float f = 0.0f;
+    if (l0 > 0.0f) { f = l0; have = true; }
+    if (l1 > 0.0f) { f = have ? fminf(f, l1) : l1; have = true; }
+    *l = f;
+    return have;
+}
+
+// Triangle::intersect, Möller–Trumbore (triangle/generic.rs:102-137)
+__device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float* l, float* bu,
+                                        float* bv) {
+    V3 e1 = v1 - v0;
+    V3 e2 = v2 - v0;
+    V3 ray_x_e2 = cross(r.d, e2);
+    float det = dot(e1, ray_x_e2);
+    if (fabsf(det) < EPS) return false;
+    float inv_det = 1.0f / det;
+    V3 rhs = r.o - v0;
+    float u = inv_det * dot(rhs, ray_x_e2);
+    if (u < 0.0f || u > 1.0f) return false;
+    V3 rhs_x_e1 = cross(rhs, e1);
+    float v = inv_det * dot(r.d, rhs_x_e1);
+    if (v < 0.0f || (u + v) > 1.0f) return false;
+    float t = inv_det * dot(e2, rhs_x_e1);
+    if (t < EPS) return false;
+    *l = t;
+    *bu = u;
+    *bv = v;
+    return true;
+}
+
+// Aabb::get_entry_exit (aabb.rs:22-62)
+__device__ __forceinline__ bool entry_exit(const float* b, const Ray& r, float* entry, float* exit_t) {
+    float vp = 0.f, wp = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float d = comp(r.d, a);
+        if (fabsf(d) < EPS) d = d < 0.0f ? -EPS : EPS;
+        float f = 1.0f / d;
+        float o = comp(r.o, a);
+        float lo = (b[2 * a] - o) * f;
+        float hi = (b[2 * a + 1] - o) * f;
+        float v = fminf(lo, hi), w = fmaxf(lo, hi);
+        if (a == 0) { vp = v; wp = w; }
+        else {
+            if (vp < v) vp = v;
+            if (wp > w) wp = w;
+        }
+    }
+    if (wp < 0.0f || vp > wp) return false;
+    *entry = vp;
+    *exit_t = wp;
+    return true;
+}
+
+// closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
+// hits not shorter than 20*EPS.
+template <bool COUNT>
+__device__ __forceinline__ bool leaf_closest(const DevScene& sc, uint32_t off, uint32_t cnt,
+                                             const Ray& r, Hit* best, Ctr<COUNT>& c) {
+    bool found = false;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        uint32_t ref = sc.refs[off + k];
+        uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
+        float l = 0.f, bu = 0.f, bv = 0.f;
+        bool h;
+        if (kind == K_SPHERE) {
+            if (COUNT) c.sph++;
+            h = sphere_hit(sc.sph[idx], r, &l);
+        } else {
+            if (COUNT) c.tri++;
+            const float4* v = sc.ftri + 3 * (size_t)idx;
+            h = tri_hit(xyz(v[0]), xyz(v[1]), xyz(v[2]), r, &l, &bu, &bv);
+        }
+        if (!h || raylen_less(l, HIT_MIN)) continue;
+        if (!found || raylen_less(l, best->l)) {
+            found = true;
+            best->ref = ref;
+            best->l = l;
+            best->bu = bu;
+            best->bv = bv;
+        }
+    }
+    return found;
+}
+
+// KdTree::closest_ray_hit + stack_search (kdtree.rs:58-104).
+template <bool COUNT>
+__device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* best,
+                                        uint32_t* st_node, float* st_t, Ctr<COUNT>& c) {
+    float root_entry, root_exit;
+    if (sc.n_nodes && entry_exit(sc.bounds, r, &root_entry, &root_exit)) {
+        float entry = root_entry, exit_t = root_exit;
+        uint32_t node = 0;
+        int sp = 0;
+        for (;;) {
+            uint2 nd = sc.nodes[node];
+            while ((nd.y & 3u) != RT_KD_LEAF) {
+                if (COUNT) c.nodes++;
+                uint32_t a = nd.y & 3u;
+                float d = comp(r.d, a);
+                if (fabsf(d) < EPS) d = d < 0.0f ? -EPS : EPS;
+                float t = (__uint_as_float(nd.x) - comp(r.o, a)) / d;
+                uint32_t low = nd.y >> 2;
+                uint32_t near = d > 0.0f ? low : low + 1;
+                uint32_t far = d > 0.0f ? low + 1 : low;
+                if (t >= exit_t) {
+                    node = near;
+                } else if (t <= entry) {
+                    node = far;
+                } else {
+                    st_node[sp * BLOCK] = far;
+                    st_t[sp * BLOCK] = t;
+                    ++sp;
+                    node = near;
+                    exit_t = t;
+                }
+                nd = sc.nodes[node];
+            }
+            if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
+            if (leaf_closest<COUNT>(sc, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
+                return true;
+            if (sp == 0) break;
+            --sp;
+            node = st_node[sp * BLOCK];
+            entry = st_t[sp * BLOCK];
+            exit_t = sp ? st_t[(sp - 1) * BLOCK] : root_exit;
+        }
+    }
+    // unconditional renderables: every cube map hits at +inf, the first one wins
+    if (sc.has_cube) {
+        best->ref = REF_CUBE;
+        best->l = __builtin_inff();
+        return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------- materials (interaction.rs)
+__device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rng); }
+
+__device__ __forceinline__ V3 spec_dir(V3 d, V3 n) {  // :6-9
+    return normalize(d - (n * 2.0f) * dot(d, n));
+}
+__device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
+    V3 xd = normalize(d - n * dot(d, n));
+    V3 yd = normalize(cross(n, xd));
+    float u = draw(rng);
+    float v = draw(rng);
+    float r = sqrtf(u);
+    float thet = 2.0f * PI * v;
+    float x = r * cosf(thet);
+    float y = r * sinf(thet);
+    return normalize((xd * x + yd * y) + n * sqrtf(fmaxf(1.0f - u, 0.0f)));
+}
+__device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, float* p,
+                                          uint32_t* rng) {  // :29-59
+    float c_ = dot(n, d);
+    bool into = c_ < 0.0f;
+    float n1 = into ? n_out : n_in, n2 = into ? n_in : n_out;
+    float c1 = into ? -c_ : c_;
+    V3 norm_refr = into ? n : -n;
+    float n_over = n1 / n2;
+    float c22 = 1.0f - n_over * n_over * (1.0f - c1 * c1);
+    V3 refl = spec_dir(d, norm_refr);
+    if (c22 < 0.0f) { *p = 1.0f; return refl; }
+    V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrtf(c22));
+    float q = (n1 - n2) / (n1 + n2);
+    float r0 = q * q;
+    float c = 1.0f - (into ? c1 : dot(trns, n));
+    float re = r0 + (1.0f + r0) * powf(c, 5.0f);
+    float u = draw(rng);
+    if (u < re) { *p = re; return refl; }
+    *p = 1.0f - re;
+    return normalize(trns);
+}
+
+// DistantCubeMap::hit_info + sample_face + UVRgb32FImage::get_pixel
+// (distant_cube_map.rs:27-69, uv_image.rs:9-23)
+__device__ __forceinline__ V3 cube_emissive(const DevScene& sc, V3 rd) {
+    int mi = 0;
+    float mc = rd.x;
+    if (fabsf(rd.y) > fabsf(mc)) { mi = 1; mc = rd.y; }
+    if (fabsf(rd.z) > fabsf(mc)) { mi = 2; mc = rd.z; }
+    if (!(mc < 0.0f) && !(mc > 0.0f)) return mk(0.f, 0.f, 0.f);
+    V3 d = normalize(rd);
+    bool neg = mc < 0.0f;
+    float u, v, fact;
+    int f;
+    if (mi == 0) { u = d.z; v = d.y; fact = d.x; f = neg ? RT_FACE_NEG_X : RT_FACE_POS_X; }
+    else if (mi == 1) { u = d.x; v = d.z; fact = d.y; f = neg ? RT_FACE_NEG_Y : RT_FACE_POS_Y; }
+    else { u = d.x; v = d.y; fact = d.z; f = neg ? RT_FACE_NEG_Z : RT_FACE_POS_Z; }
+    const DevFace fc = sc.face[f];
+    float u1 = u * fc.us / fact, v1 = v * fc.vs / fact;
+    float uu = 0.5f * u1 + 0.5f, vv = 0.5f * v1 + 0.5f;
+    float width = (float)fc.w, height = (float)fc.h;
+    float fx = fminf(fmaxf(uu * width, 0.0f), width - 1.0f);
+    float fy = fminf(fmaxf(vv * height, 0.0f), height - 1.0f);
+    uint32_t x = __builtin_isnan(fx) ? 0u : (uint32_t)truncf(fx);
+    uint32_t y = __builtin_isnan(fy) ? 0u : (uint32_t)truncf(fy);
+    return ld3(sc.texels + 3 * ((size_t)fc.off + (size_t)y * fc.w + x));
+}
+
+// ---------------------------------------------------------------- camera (generate.rs:24-66)
+__device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint32_t* rng) {
+    V3 up = ld3(sc.cam_up), right = ld3(sc.right);
+    float s_x = sc.x_cf * ((float)x - sc.x_off);
+    float s_y = sc.y_cf * ((float)y - sc.y_off);
+    V3 d = (ld3(sc.cam_d) + s_x * right) + s_y * up;
+    Ray ray;
+    if (sc.has_lens) {
+        float a = sc.lens_r;
+        float u = draw(rng);
+        float v = draw(rng);
+        float r = sqrtf(u);
+        float thet = 2.0f * PI * v;
+        float lx = (r - 0.5f) * 2.0f * a * cosf(thet);
+        float ly = (r - 0.5f) * 2.0f * a * sinf(thet);
+        V3 off = right * lx + up * ly;
+        ray.d = d - off;
+        ray.o = off + ld3(sc.cam_o);
+    } else {
+        ray.d = d;
+        ray.o = ld3(sc.cam_o);
+    }
+    float u = draw(rng) - 0.5f;
+    float v = draw(rng) - 0.5f;
+    ray.d = (ray.d + (right * u) * sc.x_cf) + (up * v) * sc.y_cf;
+    ray.d = normalize(ray.d);
+    return ray;
+}
+
+// ---------------------------------------------------------------- one sample (radiance.rs)
+template <bool COUNT>
+__device__ V3 trace_sample(const DevScene& sc, Ray ray, uint32_t* rng, uint32_t* st_node,
+                           float* st_t, Ctr<COUNT>& c) {
+    V3 L = mk(0.f, 0.f, 0.f), T = mk(1.f, 1.f, 1.f);
+    for (int depth = 0; depth < MAX_BOUNCES; ++depth) {
+        if (COUNT) c.segments++;
+        Hit h;
+        if (!closest<COUNT>(sc, ray, &h, st_node, st_t, c)) break;  // miss: radiance 0
+        if (COUNT) c.hits++;
+        if (h.ref == REF_CUBE) {  // emissive only, no continue (distant_cube_map.rs:22,52-58)
+            L = L + cmul(T, cube_emissive(sc, ray.d));
+            if (sc.debug_single_ray) break;
+            if (depth > sc.assured_depth) (void)draw(rng);  // the RR draw is still consumed
+            break;
+        }
+        const uint32_t kind = h.ref >> REF_KIND_SHIFT, idx = h.ref & REF_INDEX_MASK;
+        V3 n, pos;
+        const DevMat* m;
+        if (kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
+            float4 s = sc.sph[idx];
+            V3 perfect = ray.o + ray.d * h.l;
+            n = normalize(perfect - xyz(s));
+            pos = perfect + n * EPS;
+            m = sc.sph_mat + idx;
+        } else {  // FreeTriangle hit_info (generic.rs:78-92)
+            n = xyz(sc.ftri_n[idx]);
+            pos = (ray.d * h.l + ray.o) + n * EPS;
+            m = sc.ftri_mat + idx;
+        }
+        const uint32_t divert = m->divert;
+        bool seed_diff = false;
+        if (divert == RT_DIVERT_DIFFSPEC) seed_diff = draw(rng) < m->diffp;  // generate_seed
+        L = L + cmul(T, ld3(m->em));  // triangles carry em = 0 (generic.rs:86)
+        if (sc.debug_single_ray) break;
+        bool atten = false;  // russian_roulette_filter (radiance.rs:74-86)
+        if (depth > sc.assured_depth) {
+            if (!(draw(rng) < RR_THRES)) break;
+            atten = true;
+        }
+        float p = 1.0f;  // gen_new_ray (uniform_diff_spec.rs:44-68)
+        V3 nd;
+        if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
+            nd = spec_dir(ray.d, n);
+        } else if (divert == RT_DIVERT_DIELECTRIC) {
+            nd = refract_dir(ray.d, n, m->n_out, m->n_in, &p, rng);
+        } else {
+            nd = diff_dir(ray.d, n, rng);
+        }
+        V3 rgb = ld3(m->rgb) * p;
+        if (atten) rgb = rgb / RR_THRES;
+        T = cmul(T, rgb);
+        ray.d = nd;
+        ray.o = pos;
+    }
+    return L;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
+    __shared__ uint32_t s_node[MAX_STACK * BLOCK];
+    __shared__ float s_t[MAX_STACK * BLOCK];
+    const DevScene& sc = a.sc;
+
+    // workgroup -> tile -> 16x8 pixel block
+    uint32_t b = blockIdx.x, t = 0;
+    while (t + 1 < a.n_tiles && a.tiles[t + 1].block_begin <= b) ++t;
+    const DevTile tl = a.tiles[t];
+    const uint32_t lb = b - tl.block_begin;
+    const uint32_t lx = (lb % tl.bx) * BLOCK_W + (threadIdx.x % BLOCK_W);
+    const uint32_t ly = (lb / tl.bx) * BLOCK_H + (threadIdx.x / BLOCK_W);
+    if (lx >= tl.w || ly >= tl.h) return;
+    const int x = (int)(tl.x0 + lx), y = (int)(tl.y0 + ly);
+    const uint32_t pix = (uint32_t)y * sc.width + (uint32_t)x;
+
+    uint32_t* st_node = s_node + threadIdx.x;
+    float* st_t = s_t + threadIdx.x;
+    Ctr<COUNT> c;
+
+    V3 acc = mk(0.f, 0.f, 0.f);
+    if (a.sample_begin > 0) acc = xyz(a.accum[pix]);
+    for (uint32_t i = 0; i < a.sample_count; ++i) {
+        const uint64_t s = a.sample_begin + i;
+        uint32_t rng = rt_rng_init(sc.seed, pix, s);
+        Ray ray = camera_ray(sc, x, y, &rng);
+        V3 L = trace_sample<COUNT>(sc, ray, &rng, st_node, st_t, c);
+        const float n = (float)s;  // running mean, draw_scene.rs:81-83
+        acc = mk((L.x + (acc.x * n)) / (n + 1.0f), (L.y + (acc.y * n)) / (n + 1.0f),
+                 (L.z + (acc.z * n)) / (n + 1.0f));
+    }
+    if (COUNT) {
+        atomicAdd(&a.counts->samples, (unsigned long long)a.sample_count);
+        atomicAdd(&a.counts->segments, (unsigned long long)c.segments);
+        atomicAdd(&a.counts->nodes, (unsigned long long)c.nodes);
+        atomicAdd(&a.counts->leaf_refs, (unsigned long long)c.leaf_refs);
+        atomicAdd(&a.counts->sphere_tests, (unsigned long long)c.sph);
+        atomicAdd(&a.counts->tri_tests, (unsigned long long)c.tri);
+        atomicAdd(&a.counts->hits, (unsigned long long)c.hits);
+        atomicAdd(&a.counts->mesh_hits, (unsigned long long)c.mesh_hits);
+        return;
+    }
+    const float4 o = make_float4(acc.x, acc.y, acc.z, 1.0f);
+    a.accum[pix] = o;
+    if (a.out) a.out[tl.out_off + ly * tl.w + lx] = o;
+}
+
+hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(trace_kernel<false>, dim3(a.n_blocks), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(trace_kernel<true>, dim3(a.n_blocks), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace rtd

@@ -1,0 +1,165 @@
+"""Python host over the C ABI: what renderer.rs / draw_scene.rs do around the `use_gpu` switch.
+
+`Context` owns one rt_ctx (one device); `render_to_target` is render_to_target_gpu
+(src/render/draw_scene.rs:17-47) — spp/batch launches, RGBA8 after each, update hook.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .scheme import LoadedScheme
+
+
+def tiles_array(tiles) -> tuple:
+    arr = (abi.rt_tile * len(tiles))(*[abi.rt_tile(*map(int, t)) for t in tiles])
+    return arr, len(tiles)
+
+
+def tile_pixels(tiles) -> int:
+    return int(sum(int(t[2]) * int(t[3]) for t in tiles))
+
+
+class KdTree:
+    """A host-built KD tree (rt_kd_build) exposed as numpy views; freed on close()."""
+
+    def __init__(self, desc: abi.rt_scene_desc, max_depth: int, lib=None):
+        self.lib = lib or abi.load_library()
+        self.ptr = C.POINTER(abi.rt_kd_tree)()
+        abi.check(self.lib, self.lib.rt_kd_build(C.byref(desc), int(max_depth), C.byref(self.ptr)))
+        t = self.ptr.contents
+        self.n_nodes, self.n_refs, self.max_leaf_depth = t.n_nodes, t.n_refs, t.max_leaf_depth
+        self.bounds = np.array(list(t.bounds), dtype=np.float32)
+        nodes = np.ctypeslib.as_array(C.cast(t.nodes, C.POINTER(C.c_uint32)), shape=(t.n_nodes, 2)) if t.n_nodes else np.zeros((0, 2), np.uint32)
+        self.nodes = nodes.copy()
+        self.refs = np.ctypeslib.as_array(t.refs, shape=(t.n_refs,)).copy() if t.n_refs else np.zeros(0, np.uint32)
+        self.unconditional = (np.ctypeslib.as_array(t.unconditional, shape=(t.n_unconditional,)).copy()
+                              if t.n_unconditional else np.zeros(0, np.uint32))
+
+    def canonical_dfs(self):
+        """Depth-first pre-order rows {is_leaf, axis, split bits | count, first ref} + refs —
+        the same dump oracle_kd_dump produces from its pointer tree."""
+        rows, refs = [], []
+        if self.n_nodes == 0:
+            return np.zeros((0, 4), np.uint32), np.zeros(0, np.uint32)
+        stack = [0]
+        while stack:
+            i = stack.pop()
+            a, b = int(self.nodes[i, 0]), int(self.nodes[i, 1])
+            if (b & 3) == abi.RT_KD_LEAF:
+                off = b >> 2
+                rows.append((1, 0, a, len(refs)))
+                refs.extend(self.refs[off:off + a].tolist())
+            else:
+                rows.append((0, b & 3, a, len(refs)))
+                low = b >> 2
+                stack.append(low + 1)
+                stack.append(low)
+        return np.array(rows, dtype=np.uint32), np.array(refs, dtype=np.uint32)
+
+    def close(self):
+        if self.ptr:
+            self.lib.rt_kd_free(self.ptr)
+            self.ptr = C.POINTER(abi.rt_kd_tree)()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One rt_ctx on one gfx950 device (rt_create / rt_render / rt_destroy)."""
+
+    def __init__(self, loaded: LoadedScheme, device: int = 0, lib=None):
+        self.lib = lib or abi.load_library()
+        self.loaded = loaded
+        self.ctx = C.c_void_p()
+        st = self.lib.rt_create(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info), None,
+                                int(device), C.byref(self.ctx))
+        abi.check(self.lib, st)
+
+    @property
+    def width(self) -> int:
+        return int(self.loaded.info.width)
+
+    @property
+    def height(self) -> int:
+        return int(self.loaded.info.height)
+
+    def full_tile(self):
+        return [(0, 0, self.width, self.height)]
+
+    def render(self, tiles=None, sample_begin: int = 0, sample_count: int = 1,
+               want_output: bool = True) -> np.ndarray | None:
+        tiles = tiles or self.full_tile()
+        arr, n = tiles_array(tiles)
+        out = np.empty((tile_pixels(tiles), 4), dtype=np.float32) if want_output else None
+        ptr = out.ctypes.data_as(abi.P_f) if want_output else None
+        abi.check(self.lib, self.lib.rt_render(self.ctx, arr, n, int(sample_begin), int(sample_count), ptr),
+                  self.ctx)
+        return out
+
+    def render_device(self, dev_ptr: int, tiles=None, sample_begin: int = 0, sample_count: int = 1):
+        tiles = tiles or self.full_tile()
+        arr, n = tiles_array(tiles)
+        abi.check(self.lib, self.lib.rt_render_device(self.ctx, arr, n, int(sample_begin), int(sample_count),
+                                                      C.c_void_p(dev_ptr)), self.ctx)
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        abi.check(self.lib, self.lib.rt_last_kernel_ms(self.ctx, C.byref(ms)), self.ctx)
+        return float(ms.value)
+
+    def count_work(self, tiles=None, sample_begin: int = 0, sample_count: int = 1) -> dict:
+        tiles = tiles or self.full_tile()
+        arr, n = tiles_array(tiles)
+        wc = abi.rt_work_counts()
+        abi.check(self.lib, self.lib.rt_count_work(self.ctx, arr, n, int(sample_begin), int(sample_count),
+                                                   C.byref(wc)), self.ctx)
+        return {k: int(getattr(wc, k)) for k, _ in abi.rt_work_counts._fields_}
+
+    def close(self):
+        if self.ctx:
+            self.lib.rt_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rgba_to_u8(rgba: np.ndarray, lib=None) -> np.ndarray:
+    """rgb_f_to_u8 (draw_scene.rs:104-108) through the C++ host."""
+    lib = lib or abi.load_library()
+    rgba = np.ascontiguousarray(rgba, dtype=np.float32).reshape(-1, 4)
+    out = np.empty(rgba.shape, dtype=np.uint8)
+    abi.check(lib, lib.rt_rgba_to_u8(rgba.ctypes.data_as(abi.P_f), rgba.shape[0],
+                                     out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out
+
+
+def render_to_target(loaded: LoadedScheme, spp: int, batch: int, device: int = 0, update_hook=None,
+                     lib=None) -> np.ndarray:
+    """render_to_target_gpu (draw_scene.rs:17-47) via rt_render_to_target."""
+    lib = lib or abi.load_library()
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    target = np.zeros((h, w, 4), dtype=np.uint8)
+    HOOK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32)
+    cb = HOOK(lambda _u, done: update_hook(target, int(done))) if update_hook else None
+    st = lib.rt_render_to_target(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info), int(spp),
+                                 int(batch), int(device), target.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                 C.cast(cb, C.c_void_p) if cb else None, None)
+    abi.check(lib, st)
+    return target

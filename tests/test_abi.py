@@ -1,0 +1,104 @@
+"""The C-ABI library loads on CPU and exports every function include/rt_abi.h declares;
+ctypes mirrors match the header's layout; host-side (no GPU) entry points behave."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "rt_abi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src))
+    return {n for n in names if not n.startswith("rt_update_hook")}
+
+
+def test_exports_every_declared_symbol(rtlib):
+    from rt_amd import abi
+
+    declared = header_functions()
+    assert declared, "no functions parsed from rt_abi.h"
+    assert declared == set(abi.EXPORTS), f"mirror drift: {declared ^ set(abi.EXPORTS)}"
+    for name in declared:
+        assert hasattr(rtlib, name), name
+
+
+def test_struct_sizes_match_header():
+    from rt_amd import abi
+
+    # sizes fixed by rt_abi.h (16-byte friendly records, like assert_gpu_aligned gpu_structs.rs:18-22)
+    assert C.sizeof(abi.rt_material) == 32
+    assert C.sizeof(abi.rt_sphere) == 64
+    assert C.sizeof(abi.rt_free_triangle) == 96
+    assert C.sizeof(abi.rt_kd_node) == 8
+    assert C.sizeof(abi.rt_tile) == 16
+
+
+def test_version_and_status(rtlib):
+    assert rtlib.rt_abi_version() == 1
+    assert rtlib.rt_status_string(-6).decode().startswith("samps_per_pix")
+
+
+def test_camera_conversion_identity(rtlib):
+    from rt_amd import scheme
+
+    cam = scheme.camera({"d": [0, 0, -5.0], "o": [0, -1, 0], "up": [0, 2, 0], "view_eulers": [0, 0, 0],
+                         "screen_width": 10.0, "screen_height": 5.0})
+    assert list(cam.d) == [0.0, 0.0, -5.0]
+    assert list(cam.up) == [0.0, 1.0, 0.0]  # up normalised (builder/mod.rs:70)
+    assert cam.has_lens == 0
+
+
+def test_camera_conversion_rotation(rtlib):
+    """cam.rs:66-74: R = from_euler_angles(r, p, y) = Rz(y) Ry(p) Rx(r)."""
+    from rt_amd import scheme
+
+    e = [-0.5, 1.4, 0.0]
+    cam = scheme.camera({"d": [0, 0, 4], "o": [-30, 0, 0], "up": [0, 1, 0], "view_eulers": e,
+                         "screen_width": 10.0, "screen_height": 5.0})
+    r, p, y = e
+    Rx = np.array([[1, 0, 0], [0, np.cos(r), -np.sin(r)], [0, np.sin(r), np.cos(r)]])
+    Ry = np.array([[np.cos(p), 0, np.sin(p)], [0, 1, 0], [-np.sin(p), 0, np.cos(p)]])
+    Rz = np.array([[np.cos(y), -np.sin(y), 0], [np.sin(y), np.cos(y), 0], [0, 0, 1]])
+    R = Rz @ Ry @ Rx
+    np.testing.assert_allclose(list(cam.d), R @ [0, 0, 4], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(list(cam.up), R @ [0, 1, 0], rtol=1e-6, atol=1e-6)
+
+
+def test_rgba_to_u8_matches_rgb_f_to_u8(rtlib):
+    from rt_amd import render
+
+    vals = np.array([[0.0, 0.5, 1.0, 1.0], [-1.0, 2.0, np.nan, 1.0], [0.00196, 0.998, 0.5019608, 1.0]],
+                    dtype=np.float32)
+    out = render.rgba_to_u8(vals)
+    f = np.clip(vals[:, :3], 0, 1) * np.float32(255) + np.float32(0.5)
+    want = np.nan_to_num(np.trunc(f), nan=0).astype(np.uint8)
+    assert np.array_equal(out[:, :3], want)
+    assert np.all(out[:, 3] == 255)
+    assert out[1].tolist() == [0, 255, 0, 255]  # NaN -> 0 (Rust `as u8`)
+
+
+def test_render_to_target_rejects_bad_batch(rtlib, walled):
+    from rt_amd import abi
+
+    target = np.zeros((walled.info.height, walled.info.width, 4), np.uint8)
+    st = rtlib.rt_render_to_target(C.byref(walled.desc), C.byref(walled.cam), C.byref(walled.info), 10, 3, 0,
+                                   target.ctypes.data_as(C.POINTER(C.c_uint8)), None, None)
+    assert st == abi.RT_ERR_BATCH  # renderer.rs:56-57 panics; the ABI returns a status
+
+
+def test_create_without_device_fails_cleanly(rtlib, walled):
+    """On a machine with no gfx950 the ABI reports RT_ERR_NO_DEVICE instead of falling back."""
+    from rt_amd import abi
+
+    n = C.c_int()
+    assert rtlib.rt_device_count(C.byref(n)) == 0
+    if n.value:
+        pytest.skip("a gfx950 device is present")
+    ctx = C.c_void_p()
+    st = rtlib.rt_create(C.byref(walled.desc), C.byref(walled.cam), C.byref(walled.info), None, 0, C.byref(ctx))
+    assert st == abi.RT_ERR_NO_DEVICE and not ctx.value
