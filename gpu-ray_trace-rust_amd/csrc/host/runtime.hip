@@ -201,7 +201,8 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if ((st = upload(c, ftri_mat, &d.ftri_mat))) return st;
     if ((st = upload(c, texels, &d.texels))) return st;
     d.n_nodes = tree->n_nodes;
-    d.lds_nodes = tree->n_nodes < (uint32_t)LDS_NODES ? tree->n_nodes : (uint32_t)LDS_NODES;
+    d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
+    d.n_spheres = scene->n_spheres;
     for (int i = 0; i < 6; ++i) d.bounds[i] = tree->bounds[i];
 
     // RayCompute::new (generate.rs:13-23)

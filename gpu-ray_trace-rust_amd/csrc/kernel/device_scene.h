@@ -10,8 +10,7 @@ namespace rtd {
 constexpr int BLOCK = 128;       // threads per workgroup (2 waves): 16 x 8 pixels
 constexpr int BLOCK_W = 16;
 constexpr int BLOCK_H = 8;
-constexpr int MAX_STACK = 24;    // traversal stack entries per thread (>= max_leaf_depth)
-constexpr int LDS_NODES = 2047;  // top of the BFS-ordered node array staged in LDS (16 KiB)
+constexpr int MAX_STACK = 64;    // deepest KD tree the device path accepts (stack in LDS)
 
 // Device ref encoding: kind in the top 2 bits, index into the kind's arrays below.
 constexpr uint32_t REF_KIND_SHIFT = 30;
@@ -38,11 +37,12 @@ struct DevScene {
     const uint2* nodes;
     const uint32_t* refs;   // device-encoded refs
     uint32_t n_nodes;
-    uint32_t lds_nodes;     // min(n_nodes, LDS_NODES)
+    uint32_t stack_depth;   // traversal stack entries per lane (>= max_leaf_depth, >= 1)
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r
     const DevMat* sph_mat;
+    uint32_t n_spheres;
     // free triangles
     const float4* ftri;     // 3 per triangle: v0, v1, v2 (w unused)
     const float4* ftri_n;   // uniform normal

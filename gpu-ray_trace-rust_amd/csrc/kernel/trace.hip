@@ -8,9 +8,8 @@
 // of closest_hit.rs:6-30 -> hit_info / Russian roulette / continue_ray of the hit element
 // (sphere.rs, triangle/generic.rs, distant_cube_map.rs, material/*.rs).
 //
-// The traversal stack lives in LDS (one column per lane).  A stack entry is (far node, t):
-// the exit distance of a popped entry is the t of the entry below it (or the root exit),
-// which is what kdtree.rs:85-87 pushes, so 8 bytes per entry suffice.
+// The traversal stack lives in LDS (one column per lane), 4 bytes per entry (see closest()):
+// the branch that pushed it; t and the exit distance are recomputed on pop.
 //
 // Float order matches the oracle operation for operation (compiled with -ffp-contract=off,
 // correctly rounded div/sqrt); the only intended differences are the accumulation order of
@@ -22,6 +21,16 @@
 #include "../../../include/rt_abi.h"
 #include "../../../include/rt_rng.h"
 #include "device_scene.h"
+
+#ifndef RT_LDS_NODES
+#define RT_LDS_NODES 0      // measured: LDS-resident top nodes cost more in waves than they save
+#endif
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
+#endif
+#ifndef RT_LDS_SPHERES
+#define RT_LDS_SPHERES 64   // 1 KiB
+#endif
 
 namespace rtd {
 
@@ -79,6 +88,22 @@ template <bool COUNT>
 struct Ctr {
     uint32_t nodes = 0, leaf_refs = 0, sph = 0, tri = 0, segments = 0, hits = 0, mesh_hits = 0;
 };
+
+// Workgroup-shared copies (LDS) of the hottest scene data: the first `n_nodes` nodes of the
+// breadth-first node array (the top levels of the tree, visited by every descent) and the
+// first `n_sph` spheres.  Indices past them read HBM (through L2 / MALL).
+struct Cache {
+    const uint2* nodes;
+    uint32_t n_nodes;
+    const float4* sph;
+    uint32_t n_sph;
+};
+__device__ __forceinline__ uint2 fetch_node(const DevScene& sc, const Cache& k, uint32_t i) {
+    return i < k.n_nodes ? k.nodes[i] : sc.nodes[i];
+}
+__device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, const Cache& k, uint32_t i) {
+    return i < k.n_sph ? k.sph[i] : sc.sph[i];
+}
 
 // ---------------------------------------------------------------- primitives
 // Sphere::intersect (sphere.rs:83-105)
@@ -149,17 +174,17 @@ __device__ __forceinline__ bool entry_exit(const float* b, const Ray& r, float* 
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
 // hits not shorter than 20*EPS.
 template <bool COUNT>
-__device__ __forceinline__ bool leaf_closest(const DevScene& sc, uint32_t off, uint32_t cnt,
-                                             const Ray& r, Hit* best, Ctr<COUNT>& c) {
+__device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
+                                             uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c) {
     bool found = false;
-    for (uint32_t k = 0; k < cnt; ++k) {
-        uint32_t ref = sc.refs[off + k];
+    for (uint32_t j = 0; j < cnt; ++j) {
+        uint32_t ref = sc.refs[off + j];
         uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
         float l = 0.f, bu = 0.f, bv = 0.f;
         bool h;
         if (kind == K_SPHERE) {
             if (COUNT) c.sph++;
-            h = sphere_hit(sc.sph[idx], r, &l);
+            h = sphere_hit(fetch_sphere(sc, k, idx), r, &l);
         } else {
             if (COUNT) c.tri++;
             const float4* v = sc.ftri + 3 * (size_t)idx;
@@ -177,23 +202,38 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, uint32_t off, u
     return found;
 }
 
+// Split distance of branch `nd` along the ray (kdtree.rs:75-78): EPS-clamped direction,
+// division (not a reciprocal), so a recomputation is bit-identical to the first evaluation.
+__device__ __forceinline__ float split_t(uint2 nd, const Ray& r, float* d_out) {
+    uint32_t a = nd.y & 3u;
+    float d = comp(r.d, a);
+    if (fabsf(d) < EPS) d = d < 0.0f ? -EPS : EPS;
+    *d_out = d;
+    return (__uint_as_float(nd.x) - comp(r.o, a)) / d;
+}
+
 // KdTree::closest_ray_hit + stack_search (kdtree.rs:58-104).
+//
+// Stack: the reference pushes (far child, t, exit) (kdtree.rs:85).  Here an entry is only the
+// 4-byte index of the branch that pushed it: far child and t follow from that node and the ray
+// (split_t), and an entry's exit is the t of the entry below it (or the root exit), because
+// every push also sets exit = t.  The t of the top entry is cached in a register; popping
+// recomputes the t of the new top.  4 bytes per entry keep the LDS stack small enough that
+// LDS never limits the waves per SIMD.
 template <bool COUNT>
-__device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* best,
-                                        uint32_t* st_node, float* st_t, Ctr<COUNT>& c) {
+__device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
+                                        uint32_t* st, Ctr<COUNT>& c) {
     float root_entry, root_exit;
     if (sc.n_nodes && entry_exit(sc.bounds, r, &root_entry, &root_exit)) {
-        float entry = root_entry, exit_t = root_exit;
+        float entry = root_entry, exit_t = root_exit, top_t = root_exit;
         uint32_t node = 0;
         int sp = 0;
         for (;;) {
-            uint2 nd = sc.nodes[node];
+            uint2 nd = fetch_node(sc, k, node);
             while ((nd.y & 3u) != RT_KD_LEAF) {
                 if (COUNT) c.nodes++;
-                uint32_t a = nd.y & 3u;
-                float d = comp(r.d, a);
-                if (fabsf(d) < EPS) d = d < 0.0f ? -EPS : EPS;
-                float t = (__uint_as_float(nd.x) - comp(r.o, a)) / d;
+                float d;
+                float t = split_t(nd, r, &d);
                 uint32_t low = nd.y >> 2;
                 uint32_t near = d > 0.0f ? low : low + 1;
                 uint32_t far = d > 0.0f ? low + 1 : low;
@@ -202,22 +242,30 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* b
                 } else if (t <= entry) {
                     node = far;
                 } else {
-                    st_node[sp * BLOCK] = far;
-                    st_t[sp * BLOCK] = t;
+                    st[sp * BLOCK] = node;
                     ++sp;
+                    top_t = t;
                     node = near;
                     exit_t = t;
                 }
-                nd = sc.nodes[node];
+                nd = fetch_node(sc, k, node);
             }
             if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-            if (leaf_closest<COUNT>(sc, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
+            if (leaf_closest<COUNT>(sc, k, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
                 return true;
             if (sp == 0) break;
             --sp;
-            node = st_node[sp * BLOCK];
-            entry = st_t[sp * BLOCK];
-            exit_t = sp ? st_t[(sp - 1) * BLOCK] : root_exit;
+            uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
+            float d;
+            (void)split_t(pn, r, &d);
+            node = d > 0.0f ? (pn.y >> 2) + 1 : (pn.y >> 2);
+            entry = top_t;
+            if (sp) {
+                top_t = split_t(fetch_node(sc, k, st[(sp - 1) * BLOCK]), r, &d);
+                exit_t = top_t;
+            } else {
+                exit_t = root_exit;
+            }
         }
     }
     // unconditional renderables: every cube map hits at +inf, the first one wins
@@ -323,69 +371,113 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint
     return ray;
 }
 
-// ---------------------------------------------------------------- one sample (radiance.rs)
+// ---------------------------------------------------------------- one path segment (radiance.rs)
+// State of the path a lane is tracing: the reference's recursion (radiance.rs:20-72) unrolled
+// into L += T (x) e_k; T *= f_k.
+struct Path {
+    Ray ray;
+    V3 L, T;
+    int depth;
+    uint32_t rng;
+};
+
+// Traces one segment of `p`.  Returns true when the path has ended (miss, cube map, Russian
+// roulette, debug_single_ray, bounce cap); p.L then holds the sample's radiance.
 template <bool COUNT>
-__device__ V3 trace_sample(const DevScene& sc, Ray ray, uint32_t* rng, uint32_t* st_node,
-                           float* st_t, Ctr<COUNT>& c) {
-    V3 L = mk(0.f, 0.f, 0.f), T = mk(1.f, 1.f, 1.f);
-    for (int depth = 0; depth < MAX_BOUNCES; ++depth) {
-        if (COUNT) c.segments++;
-        Hit h;
-        if (!closest<COUNT>(sc, ray, &h, st_node, st_t, c)) break;  // miss: radiance 0
-        if (COUNT) c.hits++;
-        if (h.ref == REF_CUBE) {  // emissive only, no continue (distant_cube_map.rs:22,52-58)
-            L = L + cmul(T, cube_emissive(sc, ray.d));
-            if (sc.debug_single_ray) break;
-            if (depth > sc.assured_depth) (void)draw(rng);  // the RR draw is still consumed
-            break;
-        }
-        const uint32_t kind = h.ref >> REF_KIND_SHIFT, idx = h.ref & REF_INDEX_MASK;
-        V3 n, pos;
-        const DevMat* m;
-        if (kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
-            float4 s = sc.sph[idx];
-            V3 perfect = ray.o + ray.d * h.l;
-            n = normalize(perfect - xyz(s));
-            pos = perfect + n * EPS;
-            m = sc.sph_mat + idx;
-        } else {  // FreeTriangle hit_info (generic.rs:78-92)
-            n = xyz(sc.ftri_n[idx]);
-            pos = (ray.d * h.l + ray.o) + n * EPS;
-            m = sc.ftri_mat + idx;
-        }
-        const uint32_t divert = m->divert;
-        bool seed_diff = false;
-        if (divert == RT_DIVERT_DIFFSPEC) seed_diff = draw(rng) < m->diffp;  // generate_seed
-        L = L + cmul(T, ld3(m->em));  // triangles carry em = 0 (generic.rs:86)
-        if (sc.debug_single_ray) break;
-        bool atten = false;  // russian_roulette_filter (radiance.rs:74-86)
-        if (depth > sc.assured_depth) {
-            if (!(draw(rng) < RR_THRES)) break;
-            atten = true;
-        }
-        float p = 1.0f;  // gen_new_ray (uniform_diff_spec.rs:44-68)
-        V3 nd;
-        if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
-            nd = spec_dir(ray.d, n);
-        } else if (divert == RT_DIVERT_DIELECTRIC) {
-            nd = refract_dir(ray.d, n, m->n_out, m->n_in, &p, rng);
-        } else {
-            nd = diff_dir(ray.d, n, rng);
-        }
-        V3 rgb = ld3(m->rgb) * p;
-        if (atten) rgb = rgb / RR_THRES;
-        T = cmul(T, rgb);
-        ray.d = nd;
-        ray.o = pos;
+__device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
+                                        Ctr<COUNT>& c) {
+    if (COUNT) c.segments++;
+    Hit h;
+    if (!closest<COUNT>(sc, k, p.ray, &h, st, c)) return true;  // miss: radiance 0
+    if (COUNT) c.hits++;
+    if (h.ref == REF_CUBE) {  // emissive only, no continue (distant_cube_map.rs:22,52-58)
+        // (the reference still draws the RR uniform here; the stream ends with the path)
+        p.L = p.L + cmul(p.T, cube_emissive(sc, p.ray.d));
+        return true;
     }
-    return L;
+    const uint32_t kind = h.ref >> REF_KIND_SHIFT, idx = h.ref & REF_INDEX_MASK;
+    V3 n, pos;
+    const DevMat* m;
+    if (kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
+        float4 s = fetch_sphere(sc, k, idx);
+        V3 perfect = p.ray.o + p.ray.d * h.l;
+        n = normalize(perfect - xyz(s));
+        pos = perfect + n * EPS;
+        m = sc.sph_mat + idx;
+    } else {  // FreeTriangle hit_info (generic.rs:78-92)
+        n = xyz(sc.ftri_n[idx]);
+        pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
+        m = sc.ftri_mat + idx;
+    }
+    const uint32_t divert = m->divert;
+    bool seed_diff = false;
+    if (divert == RT_DIVERT_DIFFSPEC) seed_diff = draw(&p.rng) < m->diffp;  // generate_seed
+    p.L = p.L + cmul(p.T, ld3(m->em));  // triangles carry em = 0 (generic.rs:86)
+    if (sc.debug_single_ray) return true;
+    bool atten = false;  // russian_roulette_filter (radiance.rs:74-86)
+    if (p.depth > sc.assured_depth) {
+        if (!(draw(&p.rng) < RR_THRES)) return true;
+        atten = true;
+    }
+    float prob = 1.0f;  // gen_new_ray (uniform_diff_spec.rs:44-68)
+    V3 nd;
+    if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
+        nd = spec_dir(p.ray.d, n);
+    } else if (divert == RT_DIVERT_DIELECTRIC) {
+        nd = refract_dir(p.ray.d, n, m->n_out, m->n_in, &prob, &p.rng);
+    } else {
+        nd = diff_dir(p.ray.d, n, &p.rng);
+    }
+    V3 rgb = ld3(m->rgb) * prob;
+    if (atten) rgb = rgb / RR_THRES;
+    p.T = cmul(p.T, rgb);
+    p.ray.d = nd;
+    p.ray.o = pos;
+    return ++p.depth >= MAX_BOUNCES;
 }
 
+__device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, int y, uint32_t pix,
+                                           uint64_t s) {
+    p.rng = rt_rng_init(sc.seed, pix, s);
+    p.ray = camera_ray(sc, x, y, &p.rng);
+    p.L = mk(0.f, 0.f, 0.f);
+    p.T = mk(1.f, 1.f, 1.f);
+    p.depth = 0;
+}
+
+// One lane = one pixel for the launch's whole sample range, with path regeneration: when a
+// path ends, the lane folds its radiance into the pixel's running mean and immediately starts
+// the pixel's next sample, so a wave is not held back by its longest path of every sample
+// (lanes only idle once their own sample budget is spent).  Samples of a pixel are still
+// folded in sample order, exactly like draw_scene.rs:81-83.
 template <bool COUNT>
+#if RT_MIN_WAVES > 0
+__global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a) {
+#else
 __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
-    __shared__ uint32_t s_node[MAX_STACK * BLOCK];
-    __shared__ float s_t[MAX_STACK * BLOCK];
+#endif
+    extern __shared__ uint32_t dyn_lds[];  // traversal stack: [stack_depth][BLOCK] branch indices
+#if RT_LDS_NODES > 0
+    __shared__ uint2 s_nodes[RT_LDS_NODES];
+#endif
+#if RT_LDS_SPHERES > 0
+    __shared__ float4 s_sph[RT_LDS_SPHERES];
+#endif
     const DevScene& sc = a.sc;
+    Cache k{sc.nodes, 0, sc.sph, 0};
+#if RT_LDS_NODES > 0
+    k.nodes = s_nodes;
+    k.n_nodes = sc.n_nodes < (uint32_t)RT_LDS_NODES ? sc.n_nodes : (uint32_t)RT_LDS_NODES;
+    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) s_nodes[i] = sc.nodes[i];
+#endif
+#if RT_LDS_SPHERES > 0
+    k.sph = s_sph;
+    k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) s_sph[i] = sc.sph[i];
+#endif
+#if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
+    __syncthreads();
+#endif
 
     // workgroup -> tile -> 16x8 pixel block
     uint32_t b = blockIdx.x, t = 0;
@@ -398,20 +490,21 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     const int x = (int)(tl.x0 + lx), y = (int)(tl.y0 + ly);
     const uint32_t pix = (uint32_t)y * sc.width + (uint32_t)x;
 
-    uint32_t* st_node = s_node + threadIdx.x;
-    float* st_t = s_t + threadIdx.x;
+    uint32_t* st = dyn_lds + threadIdx.x;
     Ctr<COUNT> c;
 
     V3 acc = mk(0.f, 0.f, 0.f);
     if (a.sample_begin > 0) acc = xyz(a.accum[pix]);
-    for (uint32_t i = 0; i < a.sample_count; ++i) {
-        const uint64_t s = a.sample_begin + i;
-        uint32_t rng = rt_rng_init(sc.seed, pix, s);
-        Ray ray = camera_ray(sc, x, y, &rng);
-        V3 L = trace_sample<COUNT>(sc, ray, &rng, st_node, st_t, c);
-        const float n = (float)s;  // running mean, draw_scene.rs:81-83
-        acc = mk((L.x + (acc.x * n)) / (n + 1.0f), (L.y + (acc.y * n)) / (n + 1.0f),
-                 (L.z + (acc.z * n)) / (n + 1.0f));
+    uint32_t i = 0;
+    Path p;
+    if (a.sample_count) start_path(sc, p, x, y, pix, a.sample_begin);
+    while (i < a.sample_count) {
+        if (segment<COUNT>(sc, k, p, st, c)) {
+            const float n = (float)(a.sample_begin + i);  // running mean, draw_scene.rs:81-83
+            acc = mk((p.L.x + (acc.x * n)) / (n + 1.0f), (p.L.y + (acc.y * n)) / (n + 1.0f),
+                     (p.L.z + (acc.z * n)) / (n + 1.0f));
+            if (++i < a.sample_count) start_path(sc, p, x, y, pix, a.sample_begin + i);
+        }
     }
     if (COUNT) {
         atomicAdd(&a.counts->samples, (unsigned long long)a.sample_count);
@@ -429,12 +522,16 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     if (a.out) a.out[tl.out_off + ly * tl.w + lx] = o;
 }
 
+static size_t stack_lds_bytes(const LaunchArgs& a) {
+    return (size_t)a.sc.stack_depth * BLOCK * sizeof(uint32_t);
+}
+
 hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(trace_kernel<false>, dim3(a.n_blocks), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL(trace_kernel<false>, dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(trace_kernel<true>, dim3(a.n_blocks), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL(trace_kernel<true>, dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Collects the rocprofv3 evidence for one round on the GPU box (run through gpurun):
+#   1) kernel trace + --stats of bench.py (the committed summary),
+#   2) FETCH_SIZE (HBM read bytes; x2 on gfx950 per MI355X_MICROARCH.md §HBM) in its own pass,
+#   3) SQ occupancy / stall counters in their own pass.
+# Usage: tools/run_profiles.sh <tag> [bench args...]
+set -o pipefail
+TAG=${1:-r1}; shift
+ARGS=${@:---spp-per-step 16 --steps 5 --warmup 1}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+    python3 bench.py $ARGS --no-cpu > $OUT/bench_trace.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+    python3 bench.py $ARGS --no-cpu --no-roofline > $OUT/bench_fetch.log 2>&1 || exit 2
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d $OUT/sq -o run -- \
+    python3 bench.py $ARGS --no-cpu --no-roofline > $OUT/bench_sq.log 2>&1 || exit 3
+echo profiles_ok

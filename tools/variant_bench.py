@@ -1,0 +1,49 @@
+"""A/B timing of kernel variants in ONE process, interleaved rounds (cdna guide §5.4 rule 24).
+Usage: python tools/variant_bench.py [--scene walled] [--spp 32] [--rounds 3] name1 name2 ..."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="walled")
+    ap.add_argument("--spp", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("names", nargs="+")
+    a = ap.parse_args()
+    import torch  # noqa: F401  (owns the HIP runtime)
+    from rt_amd import abi, render, scheme
+
+    sch = scheme.load_json(os.path.join(ROOT, "tests", "golden", "scenes", a.scene + ".json"))
+    ctxs = {}
+    for n in a.names:
+        lib = abi.load_library(os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "variants", f"librt_{n}.so"))
+        loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets"), lib=lib)
+        ctxs[n] = (render.Context(loaded, lib=lib), loaded)
+    res = {n: [] for n in a.names}
+    ref = None
+    for r in range(a.rounds + 1):
+        for n, (ctx, loaded) in ctxs.items():
+            w, h = int(loaded.info.width), int(loaded.info.height)
+            t0 = time.perf_counter()
+            img = ctx.render(None, 0, a.spp, want_output=(r == 0))
+            dt = time.perf_counter() - t0
+            if r == 0:
+                if ref is None:
+                    ref = img
+                same = bool((img == ref).all())
+                print(f"{n}: identical to {a.names[0]}: {same}", flush=True)
+                continue
+            res[n].append(w * h * a.spp / (ctx.last_kernel_ms() * 1e-3) / 1e6)
+    for n, v in res.items():
+        print(json.dumps({"variant": n, "Msamples_s_kernel": [round(x, 1) for x in v], "best": round(max(v), 1)}))
+
+
+if __name__ == "__main__":
+    main()
