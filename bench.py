@@ -5,7 +5,7 @@ One step = one launch of the megakernel over this rank's pixels for `--spp-per-s
 (the reference's gpu_render_batch, walled.yml: 1000), plus — for N > 1 — the frame-end RCCL
 gather of every rank's tile radiance to rank 0.  Inputs (scene, KD tree) are resident in HBM
 before the timed region.  N GPUs: one process per GPU (torch.distributed.run), image rows
-sharded as 32-row stripes dealt round-robin.  Weak scaling: at N GPUs a step renders N x
+sharded as 4-row stripes dealt round-robin.  Weak scaling: at N GPUs a step renders N x
 spp-per-step samples for every pixel, so each rank keeps the work of the 1-GPU step
 (W*H/N pixels x N*spp samples) and the image stays bit-identical to the 1-GPU one (the RNG and
 the running mean are keyed on the global pixel and absolute sample index).
@@ -26,16 +26,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-STRIPE = 32
+STRIPE = 4  # rows; fine interleave balances sky-vs-geometry cost across ranks
 # Canonical per-event byte sizes of the roofline
 BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits": 32, "mesh_hits": 132}
 
 
 def rank_tiles(width, height, rank, world):
+    """STRIPE-row stripes dealt round-robin; consecutive stripes of one rank merge."""
     tiles = []
     for i, y0 in enumerate(range(0, height, STRIPE)):
         if i % world == rank:
-            tiles.append((0, y0, width, min(STRIPE, height - y0)))
+            hh = min(STRIPE, height - y0)
+            if tiles and tiles[-1][1] + tiles[-1][3] == y0:
+                x, yy, ww, h0 = tiles[-1]
+                tiles[-1] = (x, yy, ww, h0 + hh)
+            else:
+                tiles.append((0, y0, width, hh))
     return tiles
 
 
@@ -83,6 +89,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--as-rank", default=None,
+                    help="r/N: time rank r's share of an N-GPU run on this one GPU (no gather); "
+                         "a scaling rehearsal, not the contract's multi-process run")
     args = ap.parse_args()
 
     import torch
@@ -105,9 +114,15 @@ def main():
     loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets"))
     w, h = int(loaded.info.width), int(loaded.info.height)
     spp = args.spp_per_step or int(sch["render_info"].get("gpu_render_batch") or 1)
-    tiles = rank_tiles(w, h, rank, world)
+    shard_rank, shard_world = rank, world
+    if args.as_rank:
+        if world != 1:
+            raise SystemExit("--as-rank is a single-process rehearsal")
+        shard_rank, shard_world = (int(v) for v in args.as_rank.split("/"))
+    tiles = rank_tiles(w, h, shard_rank, shard_world)
     npix = sum(t[2] * t[3] for t in tiles)
     max_npix = max(sum(t[2] * t[3] for t in rank_tiles(w, h, r, world)) for r in range(world))
+    max_npix = max(max_npix, npix)
 
     ctx = render.Context(loaded, device=local)
     out = torch.zeros((max_npix, 4), dtype=torch.float32, device=f"cuda:{local}")
@@ -120,7 +135,7 @@ def main():
 
     sample = 0
 
-    spp_rank = spp * world  # weak scaling: per-rank work is the 1-GPU step's
+    spp_rank = spp * shard_world  # weak scaling: per-rank work is the 1-GPU step's
 
     def step():
         nonlocal sample
@@ -144,7 +159,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_samples = w * h * spp_rank * args.steps
+    total_samples = (npix if args.as_rank else w * h) * spp_rank * args.steps
     value = total_samples / elapsed / 1e6
     res = {"metric": "Msamples/s (pixels x spp / s) on walled.yml" if args.scene == "walled"
            else f"Msamples/s (pixels x spp / s) on {args.scene}.yml",
@@ -156,6 +171,9 @@ def main():
                                   f"kd_tree_depth {int(loaded.info.kd_tree_depth)}",
                       "spp_per_step": spp, "pixels": w * h, "stripes": f"{STRIPE}-row round-robin",
                       "parallelism": f"tiles{world}"}}
+    if args.as_rank:
+        res["config"]["rehearsal"] = f"rank {shard_rank} of {shard_world}, single GPU, no gather"
+        res["scaling"] = None
 
     if rank == 0 and not args.no_roofline:
         bps, trav_bps, counts = roofline_bytes_per_sample(ctx, w, h)

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -31,6 +32,10 @@ struct rt_ctx {
     float4* d_out = nullptr;
     uint64_t d_out_cap = 0;
     DevCounts* d_counts = nullptr;
+    float* radiance = nullptr;    // K > 1 sample buffer
+    uint64_t radiance_cap = 0;    // floats
+    uint64_t lane_capacity = 0;   // lanes resident at the kernel's occupancy
+    uint32_t forced_k = 0;        // RT_LANES_PER_PIXEL (tests / tuning)
     float last_ms = 0.f;
     std::string err;
 };
@@ -97,6 +102,7 @@ static void destroy_ctx(rt_ctx* c) {
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_counts) (void)hipFree(c->d_counts);
+    if (c->radiance) (void)hipFree(c->radiance);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -236,6 +242,13 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if (hipMalloc(&c->accum, npix * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "accumulator alloc failed");
     HIPCHK(c, hipMemset(c->accum, 0, npix * sizeof(float4)));
     if (hipMalloc(&c->d_counts, sizeof(DevCounts)) != hipSuccess) return set_err(c, RT_ERR_OOM, "counter alloc failed");
+    hipDeviceProp_t prop;
+    HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
+    c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
+    if (const char* e = std::getenv("RT_LANES_PER_PIXEL")) {
+        unsigned long v = std::strtoul(e, nullptr, 10);
+        if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
+    }
     return RT_OK;
 }
 
@@ -260,7 +273,7 @@ extern "C" int rt_create(const rt_scene_desc* scene, const rt_camera* cam, const
 }
 
 // Builds the per-launch tile table; returns the number of output pixels.
-static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, LaunchArgs* a,
+static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint32_t K, LaunchArgs* a,
                          uint64_t* n_out) {
     if (!tiles || n_tiles == 0) return set_err(c, RT_ERR_INVALID_ARG, "no tiles");
     std::vector<DevTile> dt(n_tiles);
@@ -274,7 +287,8 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, Laun
         d.out_off = (uint32_t)pix;
         d.block_begin = (uint32_t)blocks;
         d.bx = (t.w + BLOCK_W - 1) / BLOCK_W;
-        blocks += (uint64_t)d.bx * ((t.h + BLOCK_H - 1) / BLOCK_H);
+        const uint32_t bh = BLOCK_H / K;
+        blocks += (uint64_t)d.bx * ((t.h + bh - 1) / bh);
         pix += (uint64_t)t.w * t.h;
     }
     if (blocks >= (1ull << 31) || pix >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels");
@@ -291,21 +305,62 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, Laun
     a->n_tiles = n_tiles;
     a->n_blocks = (uint32_t)blocks;
     a->accum = c->accum;
+    a->lanes_per_pixel = K;
+    a->n_pix = (uint32_t)pix;
     *n_out = pix;
     return RT_OK;
 }
+
+static uint64_t tile_pixels(const rt_tile* tiles, uint32_t n);
+
+// Lanes per pixel: enough (pixel, sample-stream) lanes to fill the chip ~1.5x at the kernel's
+// occupancy; 1 whenever the launch has that many pixels (then samples fold in registers).
+static uint32_t choose_k(const rt_ctx* c, uint64_t n_pix) {
+    if (c->forced_k) return c->forced_k;
+    uint32_t k = 1;
+    while (k < (uint32_t)BLOCK_H && n_pix * k * 2 < c->lane_capacity * 3) k *= 2;
+    return k;
+}
+
+static int ensure_radiance(rt_ctx* c, uint64_t floats) {
+    if (floats <= c->radiance_cap) return RT_OK;
+    if (c->radiance) (void)hipFree(c->radiance);
+    c->radiance = nullptr;
+    c->radiance_cap = 0;
+    if (hipMalloc(&c->radiance, floats * sizeof(float)) != hipSuccess)
+        return set_err(c, RT_ERR_OOM, "radiance buffer alloc failed");
+    c->radiance_cap = floats;
+    return RT_OK;
+}
+
+static constexpr uint32_t SAMPLES_PER_LANE_CHUNK = 64;
 
 static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
                        uint32_t sample_count, float4* dev_out) {
     LaunchArgs a{};
     uint64_t n_out = 0;
-    int st = prepare_tiles(c, tiles, n_tiles, &a, &n_out);
+    const uint32_t K = choose_k(c, tile_pixels(tiles, n_tiles));
+    int st = prepare_tiles(c, tiles, n_tiles, K, &a, &n_out);
     if (st) return st;
-    a.sample_begin = sample_begin;
-    a.sample_count = sample_count;
     a.out = dev_out;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_trace(a, c->stream));  // count 0 still (re)writes the accumulators
+    if (K == 1) {
+        a.sample_begin = sample_begin;
+        a.sample_count = sample_count;
+        HIPCHK(c, launch_trace(a, c->stream));  // count 0 still (re)writes the accumulators
+    } else {
+        const uint32_t chunk = sample_count < SAMPLES_PER_LANE_CHUNK * K ? sample_count : SAMPLES_PER_LANE_CHUNK * K;
+        if ((st = ensure_radiance(c, 3 * n_out * (chunk ? chunk : 1)))) return st;
+        a.radiance = c->radiance;
+        uint32_t done = 0;
+        do {
+            a.sample_begin = sample_begin + done;
+            a.sample_count = sample_count - done < chunk ? sample_count - done : chunk;
+            if (a.sample_count) HIPCHK(c, launch_trace(a, c->stream));
+            HIPCHK(c, launch_fold(a, c->stream));
+            done += a.sample_count;
+        } while (done < sample_count);
+    }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     return RT_OK;
 }
@@ -364,7 +419,7 @@ extern "C" int rt_count_work(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, 
     HIPCHK(c, hipSetDevice(c->device));
     LaunchArgs a{};
     uint64_t n_out = 0;
-    int st = prepare_tiles(c, tiles, n_tiles, &a, &n_out);
+    int st = prepare_tiles(c, tiles, n_tiles, choose_k(c, tile_pixels(tiles, n_tiles)), &a, &n_out);
     if (st) return st;
     a.sample_begin = sample_begin;
     a.sample_count = sample_count;

@@ -84,10 +84,17 @@ struct LaunchArgs {
     float4* accum;          // width*height running means
     float4* out;            // tile-concatenated output (may alias nothing)
     DevCounts* counts;      // instrumented launch only
+    // K lanes per pixel (power of two <= BLOCK_H).  K == 1: each lane folds its pixel's samples
+    // in registers.  K > 1: lane k traces samples sample_begin + k + K*j into `radiance`
+    // ([sample][launch pixel] x RGB) and fold_kernel applies the running mean in sample order.
+    uint32_t lanes_per_pixel;
+    uint32_t n_pix;         // pixels of the launch (tiles concatenated)
+    float* radiance;
 };
 
 // Launch wrappers (trace.hip).
 hipError_t launch_trace(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s);
+hipError_t launch_fold(const LaunchArgs& a, hipStream_t s);
 
 }  // namespace rtd

@@ -479,35 +479,48 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     __syncthreads();
 #endif
 
-    // workgroup -> tile -> 16x8 pixel block
+    // workgroup -> tile -> block of 16 x (8/K) pixels, K lanes per pixel (adjacent lanes)
+    const uint32_t K = a.lanes_per_pixel;
     uint32_t b = blockIdx.x, t = 0;
     while (t + 1 < a.n_tiles && a.tiles[t + 1].block_begin <= b) ++t;
     const DevTile tl = a.tiles[t];
     const uint32_t lb = b - tl.block_begin;
-    const uint32_t lx = (lb % tl.bx) * BLOCK_W + (threadIdx.x % BLOCK_W);
-    const uint32_t ly = (lb / tl.bx) * BLOCK_H + (threadIdx.x / BLOCK_W);
+    const uint32_t lp = threadIdx.x / K, kk = threadIdx.x % K;
+    const uint32_t lx = (lb % tl.bx) * BLOCK_W + (lp % BLOCK_W);
+    const uint32_t ly = (lb / tl.bx) * (BLOCK_H / K) + (lp / BLOCK_W);
     if (lx >= tl.w || ly >= tl.h) return;
     const int x = (int)(tl.x0 + lx), y = (int)(tl.y0 + ly);
     const uint32_t pix = (uint32_t)y * sc.width + (uint32_t)x;
+    const uint32_t o = tl.out_off + ly * tl.w + lx;
 
     uint32_t* st = dyn_lds + threadIdx.x;
     Ctr<COUNT> c;
 
+    // this lane's samples: sample_begin + kk + K*j, j < n_mine
+    const uint32_t n_mine = kk < a.sample_count ? (a.sample_count - kk + K - 1) / K : 0;
     V3 acc = mk(0.f, 0.f, 0.f);
-    if (a.sample_begin > 0) acc = xyz(a.accum[pix]);
+    if (K == 1 && a.sample_begin > 0) acc = xyz(a.accum[pix]);
     uint32_t i = 0;
     Path p;
-    if (a.sample_count) start_path(sc, p, x, y, pix, a.sample_begin);
-    while (i < a.sample_count) {
+    if (n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk);
+    while (i < n_mine) {
         if (segment<COUNT>(sc, k, p, st, c)) {
-            const float n = (float)(a.sample_begin + i);  // running mean, draw_scene.rs:81-83
-            acc = mk((p.L.x + (acc.x * n)) / (n + 1.0f), (p.L.y + (acc.y * n)) / (n + 1.0f),
-                     (p.L.z + (acc.z * n)) / (n + 1.0f));
-            if (++i < a.sample_count) start_path(sc, p, x, y, pix, a.sample_begin + i);
+            const uint32_t rel = kk + K * i;
+            if (K == 1) {
+                const float n = (float)(a.sample_begin + rel);  // running mean, draw_scene.rs:81-83
+                acc = mk((p.L.x + (acc.x * n)) / (n + 1.0f), (p.L.y + (acc.y * n)) / (n + 1.0f),
+                         (p.L.z + (acc.z * n)) / (n + 1.0f));
+            } else if (!COUNT) {
+                float* r = a.radiance + 3 * ((size_t)rel * a.n_pix + o);
+                r[0] = p.L.x;
+                r[1] = p.L.y;
+                r[2] = p.L.z;
+            }
+            if (++i < n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk + K * i);
         }
     }
     if (COUNT) {
-        atomicAdd(&a.counts->samples, (unsigned long long)a.sample_count);
+        atomicAdd(&a.counts->samples, (unsigned long long)n_mine);
         atomicAdd(&a.counts->segments, (unsigned long long)c.segments);
         atomicAdd(&a.counts->nodes, (unsigned long long)c.nodes);
         atomicAdd(&a.counts->leaf_refs, (unsigned long long)c.leaf_refs);
@@ -517,9 +530,39 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
         atomicAdd(&a.counts->mesh_hits, (unsigned long long)c.mesh_hits);
         return;
     }
-    const float4 o = make_float4(acc.x, acc.y, acc.z, 1.0f);
-    a.accum[pix] = o;
-    if (a.out) a.out[tl.out_off + ly * tl.w + lx] = o;
+    if (K == 1) {
+        const float4 ov = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        a.accum[pix] = ov;
+        if (a.out) a.out[o] = ov;
+    }
+}
+
+// Running mean over the traced chunk, in sample order (draw_scene.rs:81-83): one lane per
+// launch pixel; reads are coalesced across lanes ([sample][pixel] layout).
+__global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
+    const uint32_t o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= a.n_pix) return;
+    uint32_t t = 0;
+    while (t + 1 < a.n_tiles && a.tiles[t + 1].out_off <= o) ++t;
+    const DevTile tl = a.tiles[t];
+    const uint32_t lo = o - tl.out_off;
+    const uint32_t pix = (tl.y0 + lo / tl.w) * a.sc.width + tl.x0 + lo % tl.w;
+    V3 acc = mk(0.f, 0.f, 0.f);
+    if (a.sample_begin > 0) acc = xyz(a.accum[pix]);
+    for (uint32_t j = 0; j < a.sample_count; ++j) {
+        const float* r = a.radiance + 3 * ((size_t)j * a.n_pix + o);
+        const float n = (float)(a.sample_begin + j);
+        acc = mk((r[0] + (acc.x * n)) / (n + 1.0f), (r[1] + (acc.y * n)) / (n + 1.0f),
+                 (r[2] + (acc.z * n)) / (n + 1.0f));
+    }
+    const float4 ov = make_float4(acc.x, acc.y, acc.z, 1.0f);
+    a.accum[pix] = ov;
+    if (a.out) a.out[o] = ov;
+}
+
+hipError_t launch_fold(const LaunchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(fold_kernel, dim3((a.n_pix + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 static size_t stack_lds_bytes(const LaunchArgs& a) {

@@ -113,3 +113,22 @@ def test_unsupported_dir_light_samp(gpu_available):
     with pytest.raises(abi.RtError) as e:
         render.Context(sc)
     assert e.value.status == abi.RT_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("k,spp", [(2, 37), (4, 37), (8, 21), (2, 300)])
+def test_lanes_per_pixel_bit_invariant(gpu_available, walled, monkeypatch, k, spp):
+    """K lanes per pixel + fold kernel (multi-GPU occupancy path) == K = 1, bit for bit,
+    including remainders and several sample chunks (300 > 64 * 2)."""
+    from rt_amd import render
+
+    crops = CROPS[:2] if spp < 100 else [(560, 260, 16, 8)]
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", "1")
+    with render.Context(walled) as c1:
+        ref = c1.render(crops, 0, spp)
+        ref2 = c1.render(crops, spp, 5)
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", str(k))
+    with render.Context(walled) as ck:
+        g = ck.render(crops, 0, spp)
+        g2 = ck.render(crops, spp, 5)
+    assert np.array_equal(g, ref)
+    assert np.array_equal(g2, ref2)
