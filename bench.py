@@ -111,7 +111,7 @@ def main():
     from rt_amd import render, scheme
 
     sch = scheme.load_json(os.path.join(ROOT, "tests", "golden", "scenes", args.scene + ".json"))
-    loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets"))
+    loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"))
     w, h = int(loaded.info.width), int(loaded.info.height)
     spp = args.spp_per_step or int(sch["render_info"].get("gpu_render_batch") or 1)
     shard_rank, shard_world = rank, world

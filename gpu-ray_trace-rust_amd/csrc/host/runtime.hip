@@ -16,6 +16,7 @@
 #include "../../../include/rt_abi.h"
 #include "../kernel/device_scene.h"
 #include "host_internal.h"
+#include "mesh_flatten.h"
 
 using namespace rtd;
 using namespace rth;
@@ -116,8 +117,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         return set_err(c, RT_ERR_INVALID_ARG, "frame too large");
     if (info->dir_light_samp)
         return set_err(c, RT_ERR_UNSUPPORTED, "dir_light_samp is not implemented on the device path");
-    if (scene->n_meshes)
-        return set_err(c, RT_ERR_UNSUPPORTED, "mesh triangles are not implemented on the device path yet");
 
     std::vector<Renderable> rs;
     int st = gather_renderables(scene, &rs);
@@ -171,9 +170,52 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         ftri_mat[i] = make_mat(t.mat, t.rgb);
     }
 
+    MeshFlat mf;
+    if ((st = flatten_meshes(scene, &mf))) return set_err(c, st, "invalid mesh description");
+    if (mf.tris.size() >= (1u << 30)) return set_err(c, RT_ERR_INVALID_ARG, "too many mesh triangles");
+    std::vector<DevPrim> prims(mf.prims.size());
+    for (size_t i = 0; i < prims.size(); ++i) {
+        const FlatPrim& f = mf.prims[i];
+        DevPrim& q = prims[i];
+        for (int k = 0; k < 3; ++k) q.base_factor[k] = f.base_factor[k];
+        q.base_tex = f.base_tex;
+        q.normal_tex = f.normal_tex;
+        q.mr_tex = f.mr_tex;
+        q.metal = f.metal;
+        q.rough = f.rough;
+    }
+    static_assert(sizeof(DevMeshTri) == sizeof(FlatTri), "mesh triangle record layout");
+    std::vector<DevMeshTri> mtri(mf.tris.size());
+    if (!mtri.empty()) std::memcpy(mtri.data(), mf.tris.data(), mtri.size() * sizeof(DevMeshTri));
+    auto as_f4 = [](const std::vector<float>& v) {
+        std::vector<float4> o(v.size() / 4);
+        for (size_t i = 0; i < o.size(); ++i) o[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        return o;
+    };
+    auto as_f2 = [](const std::vector<float>& v) {
+        std::vector<float2> o(v.size() / 2);
+        for (size_t i = 0; i < o.size(); ++i) o[i] = make_float2(v[2 * i], v[2 * i + 1]);
+        return o;
+    };
+
+    // texel pool: every scene texture, f32 RGB, in rt_scene_desc order
+    std::vector<DevTex> texs(scene->n_textures);
+    uint64_t texel_count = 0;
+    for (uint32_t i = 0; i < scene->n_textures; ++i) {
+        const rt_texture& tx = scene->textures[i];
+        if (!tx.rgb || !tx.width || !tx.height) return set_err(c, RT_ERR_INVALID_ARG, "empty texture");
+        if (texel_count + (uint64_t)tx.width * tx.height >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "texture pool too large");
+        texs[i] = DevTex{(uint32_t)texel_count, tx.width, tx.height, 0};
+        texel_count += (uint64_t)tx.width * tx.height;
+    }
+    std::vector<float> texels(3 * texel_count);
+    for (uint32_t i = 0; i < scene->n_textures; ++i) {
+        const rt_texture& tx = scene->textures[i];
+        std::memcpy(texels.data() + 3 * (size_t)texs[i].off, tx.rgb, 3 * sizeof(float) * tx.width * tx.height);
+    }
+
     DevScene& d = c->sc;
     std::memset(&d, 0, sizeof(d));
-    std::vector<float> texels;
     for (uint32_t u = 0; u < tree->n_unconditional; ++u) {
         const Renderable& r = rs[tree->unconditional[u]];
         if (r.kind != RT_KIND_CUBE_MAP) continue;
@@ -181,14 +223,11 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         for (int f = 0; f < 6; ++f) {
             int ti = cm.face[f].texture;
             if (ti < 0 || (uint32_t)ti >= scene->n_textures) return set_err(c, RT_ERR_INVALID_ARG, "bad cube face texture");
-            const rt_texture& tx = scene->textures[ti];
-            if (!tx.rgb || !tx.width || !tx.height) return set_err(c, RT_ERR_INVALID_ARG, "empty texture");
-            d.face[f].off = (uint32_t)(texels.size() / 3);
-            d.face[f].w = tx.width;
-            d.face[f].h = tx.height;
+            d.face[f].off = texs[ti].off;
+            d.face[f].w = texs[ti].w;
+            d.face[f].h = texs[ti].h;
             d.face[f].us = cm.face[f].us;
             d.face[f].vs = cm.face[f].vs;
-            texels.insert(texels.end(), tx.rgb, tx.rgb + 3 * (size_t)tx.width * tx.height);
         }
         d.has_cube = 1;
         break;  // closest_ray_hit over the unconditional list: all hit at +inf, the first wins
@@ -206,6 +245,14 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if ((st = upload(c, ftri_n, &d.ftri_n))) return st;
     if ((st = upload(c, ftri_mat, &d.ftri_mat))) return st;
     if ((st = upload(c, texels, &d.texels))) return st;
+    if ((st = upload(c, texs, &d.tex))) return st;
+    if ((st = upload(c, as_f4(mf.verts), &d.mtri_v))) return st;
+    if ((st = upload(c, mtri, &d.mtri))) return st;
+    if ((st = upload(c, prims, &d.prims))) return st;
+    if ((st = upload(c, as_f4(mf.norms), &d.vnorm))) return st;
+    if ((st = upload(c, as_f2(mf.base_uv), &d.uv_base))) return st;
+    if ((st = upload(c, as_f2(mf.normal_uv), &d.uv_norm))) return st;
+    if ((st = upload(c, as_f2(mf.mr_uv), &d.uv_mr))) return st;
     d.n_nodes = tree->n_nodes;
     d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
     d.n_spheres = scene->n_spheres;

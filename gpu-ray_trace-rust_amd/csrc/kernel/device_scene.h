@@ -32,6 +32,25 @@ struct DevFace {       // one DistantCubeMap face: texel offset, size, uv scales
     float us, vs;
 };
 
+struct DevTex {        // one UVRgb32FImage in the texel pool (f32 RGB)
+    uint32_t off, w, h, _pad;
+};
+
+struct DevPrim {       // per glTF primitive (Mesh RgbInfo / NormInfo / PbrMetalRoughInfo)
+    float base_factor[3];
+    int32_t base_tex;   // -1: factor only
+    int32_t normal_tex; // -1: interpolated vertex normals
+    int32_t mr_tex;     // -1: metal / rough factors
+    float metal, rough;
+};
+
+struct DevMeshTri {    // 64 bytes, same layout as rth::FlatTri
+    uint32_t prim;
+    uint32_t v[3];     // global vertex indices into the vertex pools
+    float m[9];        // normal transform, row-major (x normal_scale with a normal map)
+    uint32_t _pad[3];
+};
+
 struct DevScene {
     // KD tree (rt_kd_node layout), breadth-first
     const uint2* nodes;
@@ -47,10 +66,20 @@ struct DevScene {
     const float4* ftri;     // 3 per triangle: v0, v1, v2 (w unused)
     const float4* ftri_n;   // uniform normal
     const DevMat* ftri_mat;
+    // mesh triangles (src/elements/mesh)
+    const float4* mtri_v;   // 3 per triangle: pre-gathered positions
+    const DevMeshTri* mtri;
+    const DevPrim* prims;
+    const float4* vnorm;    // per global vertex
+    const float2* uv_base;
+    const float2* uv_norm;
+    const float2* uv_mr;
+    // textures
+    const DevTex* tex;
+    const float* texels;    // f32 RGB pool of every scene texture
     // cube map (first unconditional renderable, distant_cube_map.rs); has_cube == 0: misses are black
     uint32_t has_cube;
     DevFace face[6];
-    const float* texels;    // f32 RGB pool
     // camera (RayCompute, generate.rs:13-23, precomputed on host)
     float cam_d[3], cam_o[3], cam_up[3], right[3];
     float x_cf, y_cf, x_off, y_off;

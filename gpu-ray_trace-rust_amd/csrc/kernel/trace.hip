@@ -187,7 +187,7 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
             h = sphere_hit(fetch_sphere(sc, k, idx), r, &l);
         } else {
             if (COUNT) c.tri++;
-            const float4* v = sc.ftri + 3 * (size_t)idx;
+            const float4* v = (kind == K_FREE_TRI ? sc.ftri : sc.mtri_v) + 3 * (size_t)idx;
             h = tri_hit(xyz(v[0]), xyz(v[1]), xyz(v[2]), r, &l, &bu, &bv);
         }
         if (!h || raylen_less(l, HIT_MIN)) continue;
@@ -316,6 +316,22 @@ __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, f
     return normalize(trns);
 }
 
+// UVRgb32FImage::get_pixel (uv_image.rs:9-23): nearest texel, clamped, truncated; `as u32`
+// maps NaN to 0.
+__device__ __forceinline__ V3 get_pixel(const DevScene& sc, uint32_t off, uint32_t w, uint32_t h, float u,
+                                        float v) {
+    float width = (float)w, height = (float)h;
+    float fx = fminf(fmaxf(u * width, 0.0f), width - 1.0f);
+    float fy = fminf(fmaxf(v * height, 0.0f), height - 1.0f);
+    uint32_t x = __builtin_isnan(fx) ? 0u : (uint32_t)truncf(fx);
+    uint32_t y = __builtin_isnan(fy) ? 0u : (uint32_t)truncf(fy);
+    return ld3(sc.texels + 3 * ((size_t)off + (size_t)y * w + x));
+}
+__device__ __forceinline__ V3 tex_pixel(const DevScene& sc, int32_t t, float u, float v) {
+    const DevTex tx = sc.tex[t];
+    return get_pixel(sc, tx.off, tx.w, tx.h, u, v);
+}
+
 // DistantCubeMap::hit_info + sample_face + UVRgb32FImage::get_pixel
 // (distant_cube_map.rs:27-69, uv_image.rs:9-23)
 __device__ __forceinline__ V3 cube_emissive(const DevScene& sc, V3 rd) {
@@ -333,13 +349,7 @@ __device__ __forceinline__ V3 cube_emissive(const DevScene& sc, V3 rd) {
     else { u = d.x; v = d.y; fact = d.z; f = neg ? RT_FACE_NEG_Z : RT_FACE_POS_Z; }
     const DevFace fc = sc.face[f];
     float u1 = u * fc.us / fact, v1 = v * fc.vs / fact;
-    float uu = 0.5f * u1 + 0.5f, vv = 0.5f * v1 + 0.5f;
-    float width = (float)fc.w, height = (float)fc.h;
-    float fx = fminf(fmaxf(uu * width, 0.0f), width - 1.0f);
-    float fy = fminf(fmaxf(vv * height, 0.0f), height - 1.0f);
-    uint32_t x = __builtin_isnan(fx) ? 0u : (uint32_t)truncf(fx);
-    uint32_t y = __builtin_isnan(fy) ? 0u : (uint32_t)truncf(fy);
-    return ld3(sc.texels + 3 * ((size_t)fc.off + (size_t)y * fc.w + x));
+    return get_pixel(sc, fc.off, fc.w, fc.h, 0.5f * u1 + 0.5f, 0.5f * v1 + 0.5f);
 }
 
 // ---------------------------------------------------------------- camera (generate.rs:24-66)
@@ -381,6 +391,84 @@ struct Path {
     uint32_t rng;
 };
 
+// tex_coord_from_bary (mesh/triangle.rs:228-237): sum from zero of coords[i_k] * b_k.
+__device__ __forceinline__ void tex_coord(const float2* uv, const DevMeshTri& t, float b1, float b2, float* u,
+                                          float* v) {
+    float b0 = 1.0f - b2 - b1;
+    float2 c0 = uv[t.v[0]], c1 = uv[t.v[1]], c2 = uv[t.v[2]];
+    float su = 0.0f, sv = 0.0f;
+    su = su + c0.x * b0;
+    sv = sv + c0.y * b0;
+    su = su + c1.x * b1;
+    sv = sv + c1.y * b1;
+    su = su + c2.x * b2;
+    sv = sv + c2.y * b2;
+    *u = su;
+    *v = sv;
+}
+__device__ __forceinline__ V3 mul3(const float* m, V3 v) {  // nalgebra gemv order
+    return mk((m[0] * v.x + m[1] * v.y) + m[2] * v.z, (m[3] * v.x + m[4] * v.y) + m[5] * v.z,
+              (m[6] * v.x + m[7] * v.y) + m[8] * v.z);
+}
+
+// Segment ending on a mesh triangle: MeshTriangle hit_info + continue_ray
+// (triangle/generic.rs:59-92 with mesh/triangle.rs:136-225).  Draws: should_diff (1), RR (1 past
+// assured_depth), diffuse (2), roughness scatter (3).  Triangles never emit.
+template <bool COUNT>
+__device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, uint32_t idx, Path& p,
+                                          Ctr<COUNT>& c) {
+    if (COUNT) c.mesh_hits++;
+    const DevMeshTri t = sc.mtri[idx];
+    const DevPrim pr = sc.prims[t.prim];
+    const float b1 = h.bu, b2 = h.bv;
+    V3 n;  // NormFromMesh::get_norm (:136-157)
+    if (pr.normal_tex >= 0) {
+        float u, v;
+        tex_coord(sc.uv_norm, t, b1, b2, &u, &v);
+        n = normalize(mul3(t.m, tex_pixel(sc, pr.normal_tex, u, v)));
+    } else {
+        V3 cum = mk(0.f, 0.f, 0.f);
+        cum = cum + xyz(sc.vnorm[t.v[0]]);
+        cum = cum + xyz(sc.vnorm[t.v[1]]);
+        cum = cum + xyz(sc.vnorm[t.v[2]]);
+        n = normalize(mul3(t.m, cum));
+    }
+    float metal = pr.metal, rough = pr.rough;  // divert_ray_seed (:190-207)
+    if (pr.mr_tex >= 0) {
+        float u, v;
+        tex_coord(sc.uv_mr, t, b1, b2, &u, &v);
+        V3 mr = tex_pixel(sc, pr.mr_tex, u, v);
+        metal = mr.z * pr.metal;
+        rough = mr.y * pr.rough;
+    }
+    const float r0 = 0.04f + (1.0f - 0.04f) * metal;
+    const float reflectance = r0 + (1.0f - r0) * 1.0f * (1.0f - powf(fabsf(dot(p.ray.d, n)), 5.0f));
+    const bool should_diff = draw(&p.rng) < 1.0f - reflectance;  // DynDiffSpec::should_diff
+    const V3 pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
+    if (sc.debug_single_ray) return true;
+    bool atten = false;
+    if (p.depth > sc.assured_depth) {
+        if (!(draw(&p.rng) < RR_THRES)) return true;
+        atten = true;
+    }
+    V3 nd = should_diff ? diff_dir(p.ray.d, n, &p.rng) : spec_dir(p.ray.d, n);  // divert_new_ray
+    const float su = draw(&p.rng), sv = draw(&p.rng), sw = draw(&p.rng);
+    const V3 scatter = rough * normalize(mk(su, sv, sw));
+    nd = normalize(nd + scatter);
+    V3 rgb = mk(pr.base_factor[0], pr.base_factor[1], pr.base_factor[2]);  // RgbFromMesh (:166-178)
+    if (pr.base_tex >= 0) {
+        float u, v;
+        tex_coord(sc.uv_base, t, b1, b2, &u, &v);
+        rgb = cmul(rgb, tex_pixel(sc, pr.base_tex, u, v));
+    }
+    rgb = rgb * 1.0f;
+    if (atten) rgb = rgb / RR_THRES;
+    p.T = cmul(p.T, rgb);
+    p.ray.d = nd;
+    p.ray.o = pos;
+    return ++p.depth >= MAX_BOUNCES;
+}
+
 // Traces one segment of `p`.  Returns true when the path has ended (miss, cube map, Russian
 // roulette, debug_single_ray, bounce cap); p.L then holds the sample's radiance.
 template <bool COUNT>
@@ -396,6 +484,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
         return true;
     }
     const uint32_t kind = h.ref >> REF_KIND_SHIFT, idx = h.ref & REF_INDEX_MASK;
+    if (kind == K_MESH_TRI) return mesh_segment<COUNT>(sc, h, idx, p, c);
     V3 n, pos;
     const DevMat* m;
     if (kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)

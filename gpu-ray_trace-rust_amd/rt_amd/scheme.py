@@ -119,17 +119,16 @@ def resolve_asset(path: str, assets_root: str) -> str:
     return os.path.join(assets_root, *parts)
 
 
-def load_texture(path: str) -> np.ndarray:
+def load_texture(store, path: str) -> np.ndarray:
     """image::open(..).into_rgb32f() (builder/pr/distant_cube_map.rs:19-23): 8-bit channels
     -> c / 255 in f32, alpha dropped.  Decoded with PIL (JPEG decoders may differ from the
     image crate by 1 LSB — parity unpinned; oracle and device read the same texels)."""
-    from PIL import Image
+    from .assets import to_rgb32f
 
-    with Image.open(path) as im:
-        if im.mode not in ("RGB", "RGBA", "L"):
-            im = im.convert("RGBA")
-        arr = np.asarray(im.convert("RGB"), dtype=np.uint8)
-    return (arr.astype(F32) / F32(255.0)).astype(F32)
+    img = store.image(path)
+    if img is None:
+        raise FileNotFoundError(path)
+    return to_rgb32f(img)
 
 
 @dataclass
@@ -223,7 +222,10 @@ def camera(cam: dict, lib=None) -> abi.rt_camera:
 
 def scene_from_members(members: list, assets_root: str | None) -> SceneDesc:
     """Vec<Member> conversion (builder/inner.rs:21-64) in renderable order."""
+    from .assets import open_store
+
     sc = SceneDesc()
+    store = open_store(assets_root)
     tex_cache: dict[str, int] = {}
     for m in members:
         kind, v = _tag(m)
@@ -253,10 +255,9 @@ def scene_from_members(members: list, assets_root: str | None) -> SceneDesc:
             cm = abi.rt_cube_map()
             for fi, name in enumerate(("neg_x", "pos_x", "neg_y", "pos_y", "neg_z", "pos_z")):
                 path, us, vs = v[name]
-                full = resolve_asset(path, assets_root)
-                if full not in tex_cache:
-                    tex_cache[full] = sc.add_texture(load_texture(full))
-                cm.face[fi] = abi.rt_cube_face(tex_cache[full], float(_f(us)), float(_f(vs)))
+                if path not in tex_cache:
+                    tex_cache[path] = sc.add_texture(load_texture(store, path))
+                cm.face[fi] = abi.rt_cube_face(tex_cache[path], float(_f(us)), float(_f(vs)))
             sc.elems.append((abi.RT_ELEM_CUBE_MAP, len(sc.cube_maps)))
             sc.cube_maps.append(cm)
         elif kind == "Model":

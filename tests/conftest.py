@@ -11,7 +11,7 @@ for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
         sys.path.insert(0, p)
 
 SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
-ASSETS = os.path.join(ROOT, "assets")
+ASSETS = os.path.join(ROOT, "assets_pack")
 
 
 def pytest_configure(config):

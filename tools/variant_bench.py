@@ -24,7 +24,7 @@ def main():
     ctxs = {}
     for n in a.names:
         lib = abi.load_library(os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "variants", f"librt_{n}.so"))
-        loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets"), lib=lib)
+        loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"), lib=lib)
         ctxs[n] = (render.Context(loaded, lib=lib), loaded)
     res = {n: [] for n in a.names}
     ref = None
