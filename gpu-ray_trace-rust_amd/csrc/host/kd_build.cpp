@@ -3,9 +3,8 @@
 // reference's (Rust never contracts a*b+c).
 //
 // rt_kd_build restates KdTree::build / node_from_elems (src/accel/kdtree.rs:26-56,107-137)
-// iteratively and writes the 8-byte node layout of rt_abi.h directly, breadth first, so the
-// top L levels of the tree are a prefix of the node array (the device stages that prefix in
-// LDS).  The split of a node is the f32 sequential mean of its elements' AABB centroids on
+// iteratively (breadth first) into the 8-byte node layout of rt_abi.h, then re-lays the nodes
+// in 128-byte blocks (relayout_blocked) for cache-line locality on the device.  The split of a node is the f32 sequential mean of its elements' AABB centroids on
 // the node's axis (Sum<Vector3<f32>> folds from zero in element order, kdtree.rs:113); an
 // element goes high when aabb.high >= split and low when aabb.low <= split (both allowed,
 // kdtree.rs:119-127); a node is a leaf when depth > max_depth or it holds <= 1 element.
@@ -86,6 +85,56 @@ int gather_renderables(const rt_scene_desc* sc, std::vector<Renderable>* out) {
 
 using namespace rth;
 
+// Re-lays a BFS-built tree into 128-byte blocks of 16 nodes: block 0 holds the root and the
+// next three levels (1 + 2 + 4 + 8 nodes); every other block holds one sibling pair and the
+// two levels below it (2 + 4 + 8).  Children stay adjacent (low, low + 1), so the node format
+// is unchanged; a descent touches one cache line per 3 levels instead of one per level.
+static std::vector<rt_kd_node> relayout_blocked(const std::vector<rt_kd_node>& in) {
+    std::vector<rt_kd_node> out;
+    if (in.empty()) return out;
+    std::vector<uint32_t> new_of(in.size(), UINT32_MAX);
+    struct Pending { uint32_t old_first; uint32_t count; uint32_t parent_new; };  // count 1 (root) or 2
+    std::deque<Pending> q;
+    q.push_back(Pending{0, 1, UINT32_MAX});
+    auto is_leaf = [&](uint32_t i) { return (in[i].b & 3u) == RT_KD_LEAF; };
+    while (!q.empty()) {
+        Pending pb = q.front();
+        q.pop_front();
+        const uint32_t base = (uint32_t)out.size();
+        out.resize(base + 16, rt_kd_node{0, RT_KD_LEAF});  // padding slots: empty leaves, never referenced
+        const int levels = pb.count == 1 ? 4 : 3;
+        std::vector<uint32_t> level;
+        for (uint32_t k = 0; k < pb.count; ++k) level.push_back(pb.old_first + k);
+        uint32_t slot = base;
+        std::vector<uint32_t> block_nodes;
+        for (int l = 0; l < levels && !level.empty(); ++l) {
+            std::vector<uint32_t> next;
+            for (uint32_t o : level) {
+                new_of[o] = slot++;
+                block_nodes.push_back(o);
+            }
+            if (l + 1 < levels)
+                for (uint32_t o : level)
+                    if (!is_leaf(o)) { next.push_back(in[o].b >> 2); next.push_back((in[o].b >> 2) + 1); }
+            level.swap(next);
+        }
+        if (pb.parent_new != UINT32_MAX)
+            out[pb.parent_new].b = (base << 2) | (out[pb.parent_new].b & 3u);
+        for (uint32_t o : block_nodes) {
+            const uint32_t nw = new_of[o];
+            out[nw] = in[o];
+            if (is_leaf(o)) continue;
+            const uint32_t low = in[o].b >> 2;
+            if (new_of[low] != UINT32_MAX) {  // children inside this block
+                out[nw].b = (new_of[low] << 2) | (in[o].b & 3u);
+            } else {  // children start a new block; the pointer is patched when it is emitted
+                q.push_back(Pending{low, 2, nw});
+            }
+        }
+    }
+    return out;
+}
+
 struct KdTreeOwned {
     rt_kd_tree pub;
     std::vector<rt_kd_node> nodes;
@@ -156,6 +205,8 @@ extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd
             q.push_back(Item{child + 1, it.depth + 1, std::move(high)});
         }
     }
+    kt->nodes = relayout_blocked(kt->nodes);
+    if (kt->nodes.size() >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
     kt->pub.n_nodes = (uint32_t)kt->nodes.size();
     kt->pub.n_refs = (uint32_t)kt->refs.size();
     kt->pub.max_leaf_depth = max_leaf_depth;

@@ -256,6 +256,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.n_nodes = tree->n_nodes;
     d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
     d.n_spheres = scene->n_spheres;
+    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty()) ? 1u : 0u;
     for (int i = 0; i < 6; ++i) d.bounds[i] = tree->bounds[i];
 
     // RayCompute::new (generate.rs:13-23)

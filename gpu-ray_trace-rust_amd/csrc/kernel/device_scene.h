@@ -7,9 +7,12 @@
 
 namespace rtd {
 
-constexpr int BLOCK = 128;       // threads per workgroup (2 waves): 16 x 8 pixels
+#ifndef RT_BLOCK
+#define RT_BLOCK 128
+#endif
+constexpr int BLOCK = RT_BLOCK;  // threads per workgroup: 16 x (BLOCK/16) pixels at K = 1
 constexpr int BLOCK_W = 16;
-constexpr int BLOCK_H = 8;
+constexpr int BLOCK_H = BLOCK / BLOCK_W;
 constexpr int MAX_STACK = 64;    // deepest KD tree the device path accepts (stack in LDS)
 
 // Device ref encoding: kind in the top 2 bits, index into the kind's arrays below.
@@ -57,6 +60,7 @@ struct DevScene {
     const uint32_t* refs;   // device-encoded refs
     uint32_t n_nodes;
     uint32_t stack_depth;   // traversal stack entries per lane (>= max_leaf_depth, >= 1)
+    uint32_t spheres_only;  // no free / mesh triangles: launch the sphere-only kernel
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

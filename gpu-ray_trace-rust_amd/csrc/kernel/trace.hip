@@ -25,6 +25,9 @@
 #ifndef RT_LDS_NODES
 #define RT_LDS_NODES 0      // measured: LDS-resident top nodes cost more in waves than they save
 #endif
+#ifndef RT_FASTDIV
+#define RT_FASTDIV 1        // Markstein division by the per-ray reciprocal (bit-identical)
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
@@ -62,7 +65,10 @@ __device__ __forceinline__ V3 normalize(V3 a) {
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-__device__ __forceinline__ float comp(V3 v, uint32_t a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+__device__ __forceinline__ float comp(V3 v, uint32_t a) {
+    float r = __builtin_unpredictable(a == 1u) ? v.y : v.x;
+    return __builtin_unpredictable(a == 2u) ? v.z : r;
+}
 __device__ __forceinline__ V3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ V3 xyz(float4 v) { return mk(v.x, v.y, v.z); }
 
@@ -148,32 +154,9 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
 }
 
 // Aabb::get_entry_exit (aabb.rs:22-62)
-__device__ __forceinline__ bool entry_exit(const float* b, const Ray& r, float* entry, float* exit_t) {
-    float vp = 0.f, wp = 0.f;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        float d = comp(r.d, a);
-        if (fabsf(d) < EPS) d = d < 0.0f ? -EPS : EPS;
-        float f = 1.0f / d;
-        float o = comp(r.o, a);
-        float lo = (b[2 * a] - o) * f;
-        float hi = (b[2 * a + 1] - o) * f;
-        float v = fminf(lo, hi), w = fmaxf(lo, hi);
-        if (a == 0) { vp = v; wp = w; }
-        else {
-            if (vp < v) vp = v;
-            if (wp > w) wp = w;
-        }
-    }
-    if (wp < 0.0f || vp > wp) return false;
-    *entry = vp;
-    *exit_t = wp;
-    return true;
-}
-
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
 // hits not shorter than 20*EPS.
-template <bool COUNT>
+template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
                                              uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c) {
     bool found = false;
@@ -182,7 +165,7 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
         uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
         float l = 0.f, bu = 0.f, bv = 0.f;
         bool h;
-        if (kind == K_SPHERE) {
+        if (!GEN || kind == K_SPHERE) {
             if (COUNT) c.sph++;
             h = sphere_hit(fetch_sphere(sc, k, idx), r, &l);
         } else {
@@ -202,14 +185,78 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
     return found;
 }
 
-// Split distance of branch `nd` along the ray (kdtree.rs:75-78): EPS-clamped direction,
-// division (not a reciprocal), so a recomputation is bit-identical to the first evaluation.
-__device__ __forceinline__ float split_t(uint2 nd, const Ray& r, float* d_out) {
-    uint32_t a = nd.y & 3u;
-    float d = comp(r.d, a);
-    if (fabsf(d) < EPS) d = d < 0.0f ? -EPS : EPS;
+// Per-ray traversal constants: the EPS-clamped direction of kdtree.rs:75-77 / aabb.rs:28-30
+// and its correctly rounded reciprocal 1.0 / d (aabb.rs:31 computes exactly this value).
+// Named scalars, not arrays: an indexed array would be lowered to scratch memory.
+struct RayAx {
+    float dx, dy, dz, rx, ry, rz;
+};
+__device__ __forceinline__ float clamp_eps(float d) { return fabsf(d) < EPS ? (d < 0.0f ? -EPS : EPS) : d; }
+__device__ __forceinline__ RayAx ray_axes(const Ray& r) {
+    RayAx x;
+    x.dx = clamp_eps(r.d.x);
+    x.dy = clamp_eps(r.d.y);
+    x.dz = clamp_eps(r.d.z);
+    x.rx = 1.0f / x.dx;
+    x.ry = 1.0f / x.dy;
+    x.rz = 1.0f / x.dz;
+    return x;
+}
+// Branch-free pick by axis a in {0,1,2}.
+__device__ __forceinline__ float sel3(float v0, float v1, float v2, uint32_t a) {
+    float r = __builtin_unpredictable(a == 1u) ? v1 : v0;
+    return __builtin_unpredictable(a == 2u) ? v2 : r;
+}
+
+// n / d, correctly rounded.  With RT_FASTDIV: q0 = n*rcp, r = fma(-q0, d, n) (exact), q = fma(r,
+// rcp, q0).  With rcp = RN(1/d) this is RN(n/d) whenever nothing under/overflows (Markstein's
+// theorem; also checked on 2e9 random f32 pairs, tools/check_fastdiv.c); |d| is in [1e-4, 1] here
+// and numerators outside [2^-100, 2^90) (and 0) take the IEEE division.  3 instructions, not 11.
+__device__ __forceinline__ float div_exact(float n, float d, float rcp) {
+#if RT_FASTDIV
+    const uint32_t e = __float_as_uint(n) & 0x7f800000u;
+    if (__builtin_expect(e - (27u << 23) > ((216u - 27u) << 23), 0)) return n / d;
+    const float q0 = n * rcp;
+    const float res = fmaf(-q0, d, n);
+    return fmaf(res, rcp, q0);
+#else
+    (void)rcp;
+    return n / d;
+#endif
+}
+
+// Split distance of branch `nd` along the ray (kdtree.rs:75-78): (split - o_a) / d_a with the
+// clamped d, bit-identical however often it is recomputed.
+__device__ __forceinline__ float split_t(uint2 nd, const RayAx& ax, const Ray& r, float* d_out) {
+    const uint32_t a = nd.y & 3u;
+    const float d = sel3(ax.dx, ax.dy, ax.dz, a);
     *d_out = d;
-    return (__uint_as_float(nd.x) - comp(r.o, a)) / d;
+    return div_exact(__uint_as_float(nd.x) - sel3(r.o.x, r.o.y, r.o.z, a), d, sel3(ax.rx, ax.ry, ax.rz, a));
+}
+
+// Aabb::get_entry_exit (aabb.rs:22-62): slab test with the clamped direction, f = 1.0 / d.
+__device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, const Ray& r, float* entry,
+                                           float* exit_t) {
+    float vp = 0.f, wp = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float f = a == 0 ? ax.rx : (a == 1 ? ax.ry : ax.rz);
+        const float o = a == 0 ? r.o.x : (a == 1 ? r.o.y : r.o.z);
+        const float lo = (b[2 * a] - o) * f;
+        const float hi = (b[2 * a + 1] - o) * f;
+        const float v = fminf(lo, hi), w = fmaxf(lo, hi);
+        if (a == 0) {
+            vp = v;
+            wp = w;
+        } else {
+            if (vp < v) vp = v;
+            if (wp > w) wp = w;
+        }
+    }
+    if (wp < 0.0f || vp > wp) return false;
+    *entry = vp;
+    *exit_t = wp;
+    return true;
 }
 
 // KdTree::closest_ray_hit + stack_search (kdtree.rs:58-104).
@@ -220,11 +267,12 @@ __device__ __forceinline__ float split_t(uint2 nd, const Ray& r, float* d_out) {
 // every push also sets exit = t.  The t of the top entry is cached in a register; popping
 // recomputes the t of the new top.  4 bytes per entry keep the LDS stack small enough that
 // LDS never limits the waves per SIMD.
-template <bool COUNT>
+template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
     float root_entry, root_exit;
-    if (sc.n_nodes && entry_exit(sc.bounds, r, &root_entry, &root_exit)) {
+    const RayAx ax = ray_axes(r);
+    if (sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
         float entry = root_entry, exit_t = root_exit, top_t = root_exit;
         uint32_t node = 0;
         int sp = 0;
@@ -233,7 +281,7 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, cons
             while ((nd.y & 3u) != RT_KD_LEAF) {
                 if (COUNT) c.nodes++;
                 float d;
-                float t = split_t(nd, r, &d);
+                float t = split_t(nd, ax, r, &d);
                 uint32_t low = nd.y >> 2;
                 uint32_t near = d > 0.0f ? low : low + 1;
                 uint32_t far = d > 0.0f ? low + 1 : low;
@@ -251,17 +299,17 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, cons
                 nd = fetch_node(sc, k, node);
             }
             if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-            if (leaf_closest<COUNT>(sc, k, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
+            if (leaf_closest<COUNT, GEN>(sc, k, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
                 return true;
             if (sp == 0) break;
             --sp;
             uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
             float d;
-            (void)split_t(pn, r, &d);
+            (void)split_t(pn, ax, r, &d);
             node = d > 0.0f ? (pn.y >> 2) + 1 : (pn.y >> 2);
             entry = top_t;
             if (sp) {
-                top_t = split_t(fetch_node(sc, k, st[(sp - 1) * BLOCK]), r, &d);
+                top_t = split_t(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
                 exit_t = top_t;
             } else {
                 exit_t = root_exit;
@@ -471,12 +519,12 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
 
 // Traces one segment of `p`.  Returns true when the path has ended (miss, cube map, Russian
 // roulette, debug_single_ray, bounce cap); p.L then holds the sample's radiance.
-template <bool COUNT>
+template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c) {
     if (COUNT) c.segments++;
     Hit h;
-    if (!closest<COUNT>(sc, k, p.ray, &h, st, c)) return true;  // miss: radiance 0
+    if (!closest<COUNT, GEN>(sc, k, p.ray, &h, st, c)) return true;  // miss: radiance 0
     if (COUNT) c.hits++;
     if (h.ref == REF_CUBE) {  // emissive only, no continue (distant_cube_map.rs:22,52-58)
         // (the reference still draws the RR uniform here; the stream ends with the path)
@@ -484,10 +532,10 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
         return true;
     }
     const uint32_t kind = h.ref >> REF_KIND_SHIFT, idx = h.ref & REF_INDEX_MASK;
-    if (kind == K_MESH_TRI) return mesh_segment<COUNT>(sc, h, idx, p, c);
+    if (GEN && kind == K_MESH_TRI) return mesh_segment<COUNT>(sc, h, idx, p, c);
     V3 n, pos;
     const DevMat* m;
-    if (kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
+    if (!GEN || kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
         float4 s = fetch_sphere(sc, k, idx);
         V3 perfect = p.ray.o + p.ray.d * h.l;
         n = normalize(perfect - xyz(s));
@@ -539,7 +587,9 @@ __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, i
 // the pixel's next sample, so a wave is not held back by its longest path of every sample
 // (lanes only idle once their own sample budget is spent).  Samples of a pixel are still
 // folded in sample order, exactly like draw_scene.rs:81-83.
-template <bool COUNT>
+// GEN = false: the scene holds spheres only (and possibly a cube map); triangle and mesh code
+// is compiled out, which keeps the sphere kernel's register budget (walled.yml).
+template <bool COUNT, bool GEN>
 #if RT_MIN_WAVES > 0
 __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a) {
 #else
@@ -593,7 +643,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     Path p;
     if (n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk);
     while (i < n_mine) {
-        if (segment<COUNT>(sc, k, p, st, c)) {
+        if (segment<COUNT, GEN>(sc, k, p, st, c)) {
             const uint32_t rel = kk + K * i;
             if (K == 1) {
                 const float n = (float)(a.sample_begin + rel);  // running mean, draw_scene.rs:81-83
@@ -659,11 +709,17 @@ static size_t stack_lds_bytes(const LaunchArgs& a) {
 }
 
 hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(trace_kernel<false>, dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    if (a.sc.spheres_only)
+        hipLaunchKernelGGL((trace_kernel<false, false>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    else
+        hipLaunchKernelGGL((trace_kernel<false, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(trace_kernel<true>, dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    if (a.sc.spheres_only)
+        hipLaunchKernelGGL((trace_kernel<true, false>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    else
+        hipLaunchKernelGGL((trace_kernel<true, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 

@@ -20,11 +20,12 @@ def compare(scene, depth, oracle):
 
 def test_walled_full_tree(oracle, walled):
     kd = compare(walled, 17, oracle)
-    # full depth-17 tree
-    assert (kd.n_nodes, kd.n_refs, kd.max_leaf_depth) == (524287, 786443, 18)
-    leaves = (kd.nodes[:, 1] & 3) == 3
+    rows, _ = kd.canonical_dfs()
+    # full depth-17 tree (rows = reachable nodes; the array adds padding)
+    assert (len(rows), kd.n_refs, kd.max_leaf_depth) == (524287, 786443, 18)
+    leaves = rows[:, 0] == 1
     assert leaves.sum() == 262144
-    assert kd.nodes[leaves, 0].max() == 9
+    assert rows[leaves, 2].max() == 9
 
 
 @pytest.mark.parametrize("depth", [0, 1, 2, 5, 9])
@@ -32,19 +33,30 @@ def test_walled_depths(oracle, walled, depth):
     compare(walled, depth, oracle)
 
 
-def test_bfs_layout_levels_are_prefix(walled):
-    """Children are allocated in pairs in breadth-first order: the top levels form a prefix
-    of the node array (the device stages that prefix in LDS)."""
+def test_blocked_layout(walled):
+    """128-byte blocks (16 nodes): a child pair lies in its parent's block or starts a block,
+    so a root-to-leaf descent of the depth-18 tree touches at most 1 + ceil(15 / 3) = 6 lines."""
     from rt_amd import render
 
     kd = render.KdTree(walled.desc, 17)
-    depth = np.zeros(kd.n_nodes, np.int64)
-    for i in range(kd.n_nodes):
+    assert kd.n_nodes % 16 == 0
+    lines_on_path = {0: 1}
+    stack = [0]
+    worst = 0
+    while stack:
+        i = stack.pop()
         a, b = kd.nodes[i]
-        if (b & 3) != 3:
-            depth[(b >> 2)] = depth[i] + 1
-            depth[(b >> 2) + 1] = depth[i] + 1
-    assert np.all(np.diff(depth) >= 0)
+        if (b & 3) == 3:
+            worst = max(worst, lines_on_path[i])
+            continue
+        low = int(b >> 2)
+        assert low % 2 == 0 or low // 16 == i // 16
+        same = low // 16 == i // 16
+        assert same or low % 16 == 0, "a child pair outside the parent's block must start a block"
+        for c in (low, low + 1):
+            lines_on_path[c] = lines_on_path[i] + (0 if same else 1)
+            stack.append(c)
+    assert worst <= 6, worst
 
 
 def test_single_and_empty_scenes(oracle):
@@ -57,4 +69,4 @@ def test_single_and_empty_scenes(oracle):
     one["scene_members"] = one["scene_members"][:1]
     sc = scheme.load(one)
     kd = compare(sc, 17, oracle)
-    assert kd.n_nodes == 1 and kd.n_refs == 1
+    assert len(kd.canonical_dfs()[0]) == 1 and kd.n_refs == 1

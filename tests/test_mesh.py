@@ -33,8 +33,8 @@ def test_kd_equal_to_oracle(mesh_scene, oracle):
     rows, refs = kd.canonical_dfs()
     orows, orefs, ob = oracle.kd_dump(sc.desc, 17)
     assert np.array_equal(rows, orows) and np.array_equal(refs, orefs) and np.array_equal(ob, kd.bounds)
-    # SURVEY.md §8a row 6 node counts
-    assert kd.n_nodes == {"biplane": 467349, "spaceship_r1": 359075}[name]
+    # SURVEY.md §8a row 6 node counts (reachable nodes; the array adds block padding)
+    assert len(rows) == {"biplane": 467349, "spaceship_r1": 359075}[name]
 
 
 def test_normal_transforms_equal_to_oracle(mesh_scene, oracle, rtlib):

@@ -1,0 +1,75 @@
+"""Summarises a tools/run_profiles.sh output directory into profiles/<tag>_summary.md and
+copies the raw rocprofv3 CSVs that back it.  Usage: python tools/prof_summary.py <tag>"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path, kernel="trace_kernel"):
+    rows = list(csv.DictReader(open(path)))
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for r in rows:
+        if kernel in r["Kernel_Name"] and "<true" not in r["Kernel_Name"]:
+            per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"]
+    return per, names
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    lines = [f"# rocprofv3 summary — {tag}", ""]
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+        lines += ["## Kernel trace (`rocprofv3 --kernel-trace --stats`)", "", "| kernel | calls | avg ms | min ms | max ms | % |",
+                  "|---|---|---|---|---|---|"]
+        for r in csv.DictReader(open(stats)):
+            lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
+                         f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} | {r['Percentage']} |")
+        lines.append("")
+    bench = os.path.join(src, "bench_trace.log")
+    if os.path.exists(bench):
+        for l in open(bench):
+            if l.startswith("{"):
+                d = json.loads(l)
+                lines += ["## bench.py line (under the profiler)", "", "```", l.strip(), "```", ""]
+    for part, title in (("fetch", "HBM read bytes (FETCH_SIZE, own pass)"), ("sq", "SQ counters (own pass)"),
+                        ("sq2", "SQ lane utilisation (own pass)")):
+        p = os.path.join(src, part, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        shutil.copy(p, os.path.join(dst, f"{tag}_{part}_counters.csv"))
+        per, names = counters(p)
+        if not per:
+            continue
+        keys = sorted({k for d in per.values() for k in d})
+        lines += [f"## {title}", "", "| dispatch | " + " | ".join(keys) + " |", "|---" * (len(keys) + 1) + "|"]
+        for did, d in sorted(per.items(), key=lambda x: int(x[0])):
+            lines.append(f"| {did} | " + " | ".join(f"{d[k]:.4g}" for k in keys) + " |")
+        d = list(per.values())[-1]
+        if "FETCH_SIZE" in d:
+            lines.append(f"\nLast dispatch: FETCH_SIZE {d['FETCH_SIZE']:.1f} KB -> x2 (gfx950 correction) = "
+                         f"{2 * d['FETCH_SIZE'] / 1024:.2f} MB read from HBM per launch.")
+        if "SQ_WAVE_CYCLES" in d:
+            wc = d["SQ_WAVE_CYCLES"]
+            lines.append(f"\nLast dispatch: wait-any {d.get('SQ_WAIT_ANY', 0) / wc:.1%}, issuing {d.get('SQ_ACTIVE_INST_ANY', 0) / wc:.1%}, "
+                         f"issue-stall {d.get('SQ_WAIT_INST_ANY', 0) / wc:.1%} of wave cycles.")
+        if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
+            lines.append(f"\nLast dispatch: VALU lane utilisation = THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU) = "
+                         f"{d['SQ_THREAD_CYCLES_VALU'] / (64 * d['SQ_ACTIVE_INST_VALU']):.1%}.")
+        lines.append("")
+    out = os.path.join(dst, f"{tag}_summary.md")
+    open(out, "w").write("\n".join(lines) + "\n")
+    print(open(out).read())
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -2,11 +2,11 @@
 # Collects the rocprofv3 evidence for one round on the GPU box (run through gpurun):
 #   1) kernel trace + --stats of bench.py (the committed summary),
 #   2) FETCH_SIZE (HBM read bytes; x2 on gfx950 per MI355X_MICROARCH.md §HBM) in its own pass,
-#   3) SQ occupancy / stall counters in their own pass.
+#   3) SQ occupancy / stall / lane-utilisation counters in their own passes.
 # Usage: tools/run_profiles.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r1}; shift
-ARGS=${@:---spp-per-step 16 --steps 5 --warmup 1}
+ARGS=${@:---spp-per-step 64 --steps 3 --warmup 1}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
@@ -16,4 +16,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
     python3 bench.py $ARGS --no-cpu --no-roofline > $OUT/bench_fetch.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d $OUT/sq -o run -- \
     python3 bench.py $ARGS --no-cpu --no-roofline > $OUT/bench_sq.log 2>&1 || exit 3
+timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $OUT/sq2 -o run -- \
+    python3 bench.py $ARGS --no-cpu --no-roofline > $OUT/bench_sq2.log 2>&1 || echo "sq2 pass failed (counter set)"
 echo profiles_ok
