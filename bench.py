@@ -55,6 +55,22 @@ def roofline_bytes_per_sample(ctx, width, height, spp=16):
     return total / c["samples"], trav / c["samples"], c
 
 
+def committed_traffic(scene, spp_rank, npix):
+    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE pass of the same workload
+    (profiles/*_fetch.json, written by tools/prof_summary.py), or None."""
+    import glob
+
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_fetch.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("scene") == scene and d.get("samples_per_launch") == spp_rank * npix:
+            best = (d["hbm_read_bytes_per_launch"], os.path.relpath(p, ROOT))
+    return best
+
+
 def cpu_baseline(loaded, target_s=10.0, threads=None):
     """The oracle (C++ restatement of render_to_target_cpu) on this host's cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -62,12 +78,13 @@ def cpu_baseline(loaded, target_s=10.0, threads=None):
 
     threads = threads or min(16, os.cpu_count() or 1)
     w, h = int(loaded.info.width), int(loaded.info.height)
-    # calibrate on a band of rows, then run a sample sized for ~target_s
-    band = [(0, 0, w, 64)]
+    # calibrate on every 8th row (representative of the frame's cost mix), then run a sample
+    # sized for ~target_s of CPU time
+    rows = [(0, y, w, 1) for y in range(0, h, 8)]
     t0 = time.perf_counter()
-    oracle_py.render(loaded, band, 0, 1, threads=threads)
+    oracle_py.render(loaded, rows, 0, 2, threads=threads)
     dt = max(time.perf_counter() - t0, 1e-3)
-    rate = w * 64 / dt
+    rate = w * len(rows) * 2 / dt
     spp = max(1, min(64, int(target_s * rate / (w * h))))
     t0 = time.perf_counter()
     oracle_py.render(loaded, [(0, 0, w, h)], 0, spp, threads=threads)
@@ -179,9 +196,16 @@ def main():
         bps, trav_bps, counts = roofline_bytes_per_sample(ctx, w, h)
         avg_ms = sum(kernel_ms) / len(kernel_ms)
         achieved = bps * npix * spp_rank / (avg_ms * 1e-3) / 1e9
+        spheres_only = loaded.desc.n_free_tris == 0 and loaded.desc.n_meshes == 0
+        traffic = committed_traffic(args.scene, spp_rank, npix)
         res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                           "kernel": "trace_kernel<false>", "kernel_ms_avg": round(avg_ms, 3),
+                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                           "traffic": traffic[0] if traffic else None,
+                           "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2, gfx950)",
+                           "traffic_source": traffic[1] if traffic else None,
+                           "algorithmic_bytes_per_launch": round(bps * npix * spp_rank),
+                           "kernel": f"rtd::trace_kernel<false, {'false' if spheres_only else 'true'}>",
+                           "kernel_ms_avg": round(avg_ms, 3),
                            "bytes_per_sample": round(bps, 1), "traversal_bytes_per_sample": round(trav_bps, 1),
                            "samples_per_launch": npix * spp_rank,
                            "counts_per_sample": {k: round(v / counts["samples"], 3) for k, v in counts.items()
