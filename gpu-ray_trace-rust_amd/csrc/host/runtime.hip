@@ -254,6 +254,12 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if ((st = upload(c, as_f2(mf.normal_uv), &d.uv_norm))) return st;
     if ((st = upload(c, as_f2(mf.mr_uv), &d.uv_mr))) return st;
     d.n_nodes = tree->n_nodes;
+    d.fastdiv = 1;  // see trace.hip div_exact: splits must be 0 or in [2^-70, 2^61)
+    for (uint32_t i = 0; i < tree->n_nodes; ++i) {
+        if ((tree->nodes[i].b & 3u) == RT_KD_LEAF) continue;
+        const uint32_t m = tree->nodes[i].a & 0x7fffffffu;
+        if (m != 0u && (m < (57u << 23) || m >= (188u << 23))) d.fastdiv = 0;
+    }
     d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
     d.n_spheres = scene->n_spheres;
     d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty()) ? 1u : 0u;

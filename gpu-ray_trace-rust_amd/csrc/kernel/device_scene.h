@@ -61,6 +61,7 @@ struct DevScene {
     uint32_t n_nodes;
     uint32_t stack_depth;   // traversal stack entries per lane (>= max_leaf_depth, >= 1)
     uint32_t spheres_only;  // no free / mesh triangles: launch the sphere-only kernel
+    uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

@@ -208,30 +208,38 @@ __device__ __forceinline__ float sel3(float v0, float v1, float v2, uint32_t a) 
     return __builtin_unpredictable(a == 2u) ? v2 : r;
 }
 
-// n / d, correctly rounded.  With RT_FASTDIV: q0 = n*rcp, r = fma(-q0, d, n) (exact), q = fma(r,
-// rcp, q0).  With rcp = RN(1/d) this is RN(n/d) whenever nothing under/overflows (Markstein's
-// theorem; also checked on 2e9 random f32 pairs, tools/check_fastdiv.c); |d| is in [1e-4, 1] here
-// and numerators outside [2^-100, 2^90) (and 0) take the IEEE division.  3 instructions, not 11.
+// n / d, correctly rounded.  FAST: q0 = n*rcp, r = fma(-q0, d, n) (exact), q = fma(r, rcp, q0).
+// With rcp = RN(1/d) this is RN(n/d) whenever nothing under/overflows (Markstein's theorem; also
+// checked on 2e9 random f32 pairs, tools/check_fastdiv.c): 3 instructions instead of 11.  Here
+// |d| is in [1e-4, 1] and FAST is only used when every split and ray-origin component is 0 or in
+// [2^-70, 2^60] (origin_fast_ok, DevScene::fastdiv), so |n| = |split - o| is 0 or in
+// [2^-93, 2^61]: no intermediate under/overflows.
+template <bool FAST>
 __device__ __forceinline__ float div_exact(float n, float d, float rcp) {
-#if RT_FASTDIV
-    const uint32_t e = __float_as_uint(n) & 0x7f800000u;
-    if (__builtin_expect(e - (27u << 23) > ((216u - 27u) << 23), 0)) return n / d;
-    const float q0 = n * rcp;
-    const float res = fmaf(-q0, d, n);
-    return fmaf(res, rcp, q0);
-#else
+    if (FAST) {
+        const float q0 = n * rcp;
+        const float res = fmaf(-q0, d, n);
+        return fmaf(res, rcp, q0);
+    }
     (void)rcp;
     return n / d;
-#endif
+}
+__device__ __forceinline__ bool fast_range(float x) {
+    const uint32_t b = __float_as_uint(x) & 0x7fffffffu;
+    return b == 0u || (b >= (57u << 23) && b < (188u << 23));  // 0 or [2^-70, 2^61)
+}
+__device__ __forceinline__ bool origin_fast_ok(V3 o) {
+    return fast_range(o.x) && fast_range(o.y) && fast_range(o.z);
 }
 
 // Split distance of branch `nd` along the ray (kdtree.rs:75-78): (split - o_a) / d_a with the
 // clamped d, bit-identical however often it is recomputed.
+template <bool FAST>
 __device__ __forceinline__ float split_t(uint2 nd, const RayAx& ax, const Ray& r, float* d_out) {
     const uint32_t a = nd.y & 3u;
     const float d = sel3(ax.dx, ax.dy, ax.dz, a);
     *d_out = d;
-    return div_exact(__uint_as_float(nd.x) - sel3(r.o.x, r.o.y, r.o.z, a), d, sel3(ax.rx, ax.ry, ax.rz, a));
+    return div_exact<FAST>(__uint_as_float(nd.x) - sel3(r.o.x, r.o.y, r.o.z, a), d, sel3(ax.rx, ax.ry, ax.rz, a));
 }
 
 // Aabb::get_entry_exit (aabb.rs:22-62): slab test with the clamped direction, f = 1.0 / d.
@@ -259,7 +267,7 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
     return true;
 }
 
-// KdTree::closest_ray_hit + stack_search (kdtree.rs:58-104).
+// KdTree::stack_search (kdtree.rs:66-104) from the root interval [root_entry, root_exit].
 //
 // Stack: the reference pushes (far child, t, exit) (kdtree.rs:85).  Here an entry is only the
 // 4-byte index of the branch that pushed it: far child and t follow from that node and the ray
@@ -267,54 +275,71 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
 // every push also sets exit = t.  The t of the top entry is cached in a register; popping
 // recomputes the t of the new top.  4 bytes per entry keep the LDS stack small enough that
 // LDS never limits the waves per SIMD.
+//
+// The descent step is branch-free: the current branch is always written to slot sp (above the
+// stack top when nothing is pushed; a branch at depth D has sp <= D < stack_depth) and sp only
+// advances on a push, so the three reference cases (near / far / push both) are selects.
+template <bool COUNT, bool GEN, bool FAST>
+__device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
+                                             float root_entry, float root_exit, Hit* best, uint32_t* st,
+                                             Ctr<COUNT>& c) {
+    float entry = root_entry, exit_t = root_exit, top_t = root_exit;
+    uint32_t node = 0;
+    int sp = 0;
+    for (;;) {
+        uint2 nd = fetch_node(sc, k, node);
+        while ((nd.y & 3u) != RT_KD_LEAF) {
+            if (COUNT) c.nodes++;
+            float d;
+            const float t = split_t<FAST>(nd, ax, r, &d);
+            const bool pos = d > 0.0f;          // near = low when d > 0 (kdtree.rs:79)
+            const bool go_near = t >= exit_t;   // kdtree.rs:80
+            const bool go_far = !go_near && t <= entry;  // kdtree.rs:82
+            const bool push = !go_near && !go_far;       // kdtree.rs:84-87
+            st[sp * BLOCK] = node;
+            sp += push ? 1 : 0;
+            top_t = push ? t : top_t;
+            exit_t = push ? t : exit_t;
+            node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
+            nd = fetch_node(sc, k, node);
+        }
+        if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
+        if (leaf_closest<COUNT, GEN>(sc, k, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
+            return true;
+        if (sp == 0) return false;
+        --sp;
+        const uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
+        float d;
+        (void)split_t<FAST>(pn, ax, r, &d);
+        node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);  // the far child
+        entry = top_t;
+        if (sp) {
+            top_t = split_t<FAST>(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
+            exit_t = top_t;
+        } else {
+            exit_t = root_exit;
+        }
+    }
+}
+
+// KdTree::closest_ray_hit (kdtree.rs:58-64): root slab test, stack search, then the
+// unconditional renderables.  The Markstein division is used for the whole wave unless some
+// lane's origin (or the scene's splits) could underflow it.
 template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
-        float entry = root_entry, exit_t = root_exit, top_t = root_exit;
-        uint32_t node = 0;
-        int sp = 0;
-        for (;;) {
-            uint2 nd = fetch_node(sc, k, node);
-            while ((nd.y & 3u) != RT_KD_LEAF) {
-                if (COUNT) c.nodes++;
-                float d;
-                float t = split_t(nd, ax, r, &d);
-                uint32_t low = nd.y >> 2;
-                uint32_t near = d > 0.0f ? low : low + 1;
-                uint32_t far = d > 0.0f ? low + 1 : low;
-                if (t >= exit_t) {
-                    node = near;
-                } else if (t <= entry) {
-                    node = far;
-                } else {
-                    st[sp * BLOCK] = node;
-                    ++sp;
-                    top_t = t;
-                    node = near;
-                    exit_t = t;
-                }
-                nd = fetch_node(sc, k, node);
-            }
-            if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-            if (leaf_closest<COUNT, GEN>(sc, k, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
-                return true;
-            if (sp == 0) break;
-            --sp;
-            uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
-            float d;
-            (void)split_t(pn, ax, r, &d);
-            node = d > 0.0f ? (pn.y >> 2) + 1 : (pn.y >> 2);
-            entry = top_t;
-            if (sp) {
-                top_t = split_t(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
-                exit_t = top_t;
-            } else {
-                exit_t = root_exit;
-            }
-        }
+        bool found;
+#if RT_FASTDIV
+        const bool fast = sc.fastdiv && origin_fast_ok(r.o);
+        if (__builtin_expect(__ballot(!fast) == 0, 1))
+            found = stack_search<COUNT, GEN, true>(sc, k, r, ax, root_entry, root_exit, best, st, c);
+        else
+#endif
+            found = stack_search<COUNT, GEN, false>(sc, k, r, ax, root_entry, root_exit, best, st, c);
+        if (found) return true;
     }
     // unconditional renderables: every cube map hits at +inf, the first one wins
     if (sc.has_cube) {
