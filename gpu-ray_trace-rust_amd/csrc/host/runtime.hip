@@ -15,6 +15,9 @@
 
 #include "../../../include/rt_abi.h"
 #include "../kernel/device_scene.h"
+#ifndef RT_LDS_SPHERES
+#define RT_LDS_SPHERES 64  // must match trace.hip
+#endif
 #include "host_internal.h"
 #include "mesh_flatten.h"
 
@@ -262,7 +265,8 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
     d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
     d.n_spheres = scene->n_spheres;
-    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty()) ? 1u : 0u;
+    // the sphere-only kernel reads every sphere from its LDS table (trace.hip fetch_sphere)
+    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty() && scene->n_spheres <= RT_LDS_SPHERES) ? 1u : 0u;
     for (int i = 0; i < 6; ++i) d.bounds[i] = tree->bounds[i];
 
     // RayCompute::new (generate.rs:13-23)

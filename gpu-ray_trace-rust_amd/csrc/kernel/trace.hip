@@ -98,36 +98,51 @@ struct Ctr {
 // Workgroup-shared copies (LDS) of the hottest scene data: the first `n_nodes` nodes of the
 // breadth-first node array (the top levels of the tree, visited by every descent) and the
 // first `n_sph` spheres.  Indices past them read HBM (through L2 / MALL).
+// The LDS copies are file-scope __shared__ arrays referenced directly, so loads from them are
+// ds_read (a pointer that may be LDS or global would become a slower FLAT load).
+#if RT_LDS_NODES > 0
+__shared__ uint2 g_lds_nodes[RT_LDS_NODES];
+#endif
+#if RT_LDS_SPHERES > 0
+__shared__ float4 g_lds_sph[RT_LDS_SPHERES];
+#endif
 struct Cache {
-    const uint2* nodes;
-    uint32_t n_nodes;
-    const float4* sph;
-    uint32_t n_sph;
+    uint32_t n_nodes;  // nodes [0, n_nodes) are in g_lds_nodes
+    uint32_t n_sph;    // spheres [0, n_sph) are in g_lds_sph
 };
 __device__ __forceinline__ uint2 fetch_node(const DevScene& sc, const Cache& k, uint32_t i) {
-    return i < k.n_nodes ? k.nodes[i] : sc.nodes[i];
+#if RT_LDS_NODES > 0
+    if (i < k.n_nodes) return g_lds_nodes[i];
+#endif
+    (void)k;
+    return sc.nodes[i];
 }
+// GEN == false (sphere-only kernel, launched only when every sphere fits the LDS table):
+// spheres come from LDS only.  The general kernel reads them from global memory.
+template <bool GEN>
 __device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, const Cache& k, uint32_t i) {
-    return i < k.n_sph ? k.sph[i] : sc.sph[i];
+    (void)k;
+#if RT_LDS_SPHERES > 0
+    if (!GEN) return g_lds_sph[i];
+#endif
+    return sc.sph[i];
 }
 
 // ---------------------------------------------------------------- primitives
 // Sphere::intersect (sphere.rs:83-105)
+// Branch-free: sqrt of max(thing2, 0) equals sqrt(thing2) whenever the hit is taken.
 __device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
-    V3 oc = r.o - xyz(s);
-    float dir = dot(r.d, oc);
-    float consts = dot(oc, oc) - s.w * s.w;
-    float thing2 = dir * dir - consts;
-    if (!(thing2 > 0.0f)) return false;
-    float offset = -dir;
-    float thing = sqrtf(thing2);
-    float l0 = offset + thing, l1 = offset - thing;
-    bool have = false;
-    float f = 0.0f;
-    if (l0 > 0.0f) { f = l0; have = true; }
-    if (l1 > 0.0f) { f = have ? fminf(f, l1) : l1; have = true; }
-    *l = f;
-    return have;
+    const V3 oc = r.o - xyz(s);
+    const float dir = dot(r.d, oc);
+    const float consts = dot(oc, oc) - s.w * s.w;
+    const float thing2 = dir * dir - consts;
+    const bool disc = thing2 > 0.0f;
+    const float offset = -dir;
+    const float thing = sqrtf(fmaxf(thing2, 0.0f));
+    const float l0 = offset + thing, l1 = offset - thing;
+    const bool p0 = l0 > 0.0f, p1 = l1 > 0.0f;
+    *l = p0 ? (p1 ? fminf(l0, l1) : l0) : l1;  // filter(>0).reduce(min), sphere.rs:95
+    return disc && (p0 || p1);
 }
 
 // Triangle::intersect, Möller–Trumbore (triangle/generic.rs:102-137)
@@ -167,20 +182,21 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
         bool h;
         if (!GEN || kind == K_SPHERE) {
             if (COUNT) c.sph++;
-            h = sphere_hit(fetch_sphere(sc, k, idx), r, &l);
+            h = sphere_hit(fetch_sphere<GEN>(sc, k, idx), r, &l);
         } else {
             if (COUNT) c.tri++;
             const float4* v = (kind == K_FREE_TRI ? sc.ftri : sc.mtri_v) + 3 * (size_t)idx;
             h = tri_hit(xyz(v[0]), xyz(v[1]), xyz(v[2]), r, &l, &bu, &bv);
         }
-        if (!h || raylen_less(l, HIT_MIN)) continue;
-        if (!found || raylen_less(l, best->l)) {
-            found = true;
-            best->ref = ref;
-            best->l = l;
-            best->bu = bu;
-            best->bv = bv;
-        }
+        // spheres never produce a NaN length: plain compares; triangles keep RayLen's order
+        const bool above = GEN ? !raylen_less(l, HIT_MIN) : !(l < HIT_MIN);
+        const bool closer = GEN ? raylen_less(l, best->l) : (l < best->l);
+        const bool take = h & above & (!found | closer);
+        best->ref = take ? ref : best->ref;
+        best->l = take ? l : best->l;
+        best->bu = take ? bu : best->bu;
+        best->bv = take ? bv : best->bv;
+        found = found || take;
     }
     return found;
 }
@@ -561,7 +577,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
     V3 n, pos;
     const DevMat* m;
     if (!GEN || kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
-        float4 s = fetch_sphere(sc, k, idx);
+        float4 s = fetch_sphere<GEN>(sc, k, idx);
         V3 perfect = p.ray.o + p.ray.d * h.l;
         n = normalize(perfect - xyz(s));
         pos = perfect + n * EPS;
@@ -621,23 +637,15 @@ __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a
 __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
 #endif
     extern __shared__ uint32_t dyn_lds[];  // traversal stack: [stack_depth][BLOCK] branch indices
-#if RT_LDS_NODES > 0
-    __shared__ uint2 s_nodes[RT_LDS_NODES];
-#endif
-#if RT_LDS_SPHERES > 0
-    __shared__ float4 s_sph[RT_LDS_SPHERES];
-#endif
     const DevScene& sc = a.sc;
-    Cache k{sc.nodes, 0, sc.sph, 0};
+    Cache k{0, 0};
 #if RT_LDS_NODES > 0
-    k.nodes = s_nodes;
     k.n_nodes = sc.n_nodes < (uint32_t)RT_LDS_NODES ? sc.n_nodes : (uint32_t)RT_LDS_NODES;
-    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) s_nodes[i] = sc.nodes[i];
+    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
 #endif
 #if RT_LDS_SPHERES > 0
-    k.sph = s_sph;
     k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) s_sph[i] = sc.sph[i];
+    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
 #endif
 #if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
     __syncthreads();
