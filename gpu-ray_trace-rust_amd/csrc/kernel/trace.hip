@@ -28,6 +28,9 @@
 #ifndef RT_FASTDIV
 #define RT_FASTDIV 1        // Markstein division by the per-ray reciprocal (bit-identical)
 #endif
+#ifndef RT_SMALL_SCENE
+#define RT_SMALL_SCENE 1    // exact brute-force-bounded traversal for <= 32 spheres (closest_small)
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
@@ -171,13 +174,17 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
 // Aabb::get_entry_exit (aabb.rs:22-62)
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
 // hits not shorter than 20*EPS.
-template <bool COUNT, bool GEN>
+// SMALL: `mask` has bit i set iff sphere i has a valid hit (closest_small); other spheres
+// cannot be the leaf's candidate and are not re-tested.
+template <bool COUNT, bool GEN, bool SMALL = false>
 __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
-                                             uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c) {
+                                             uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c,
+                                             uint32_t mask = 0) {
     bool found = false;
     for (uint32_t j = 0; j < cnt; ++j) {
         uint32_t ref = sc.refs[off + j];
         uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
+        if (SMALL && !((mask >> idx) & 1u)) continue;
         float l = 0.f, bu = 0.f, bv = 0.f;
         bool h;
         if (!GEN || kind == K_SPHERE) {
@@ -295,10 +302,10 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
 // The descent step is branch-free: the current branch is always written to slot sp (above the
 // stack top when nothing is pushed; a branch at depth D has sp <= D < stack_depth) and sp only
 // advances on a push, so the three reference cases (near / far / push both) are selects.
-template <bool COUNT, bool GEN, bool FAST>
+template <bool COUNT, bool GEN, bool FAST, bool SMALL = false>
 __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
                                              float root_entry, float root_exit, Hit* best, uint32_t* st,
-                                             Ctr<COUNT>& c) {
+                                             Ctr<COUNT>& c, uint32_t mask = 0) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0;
     int sp = 0;
@@ -320,7 +327,7 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
             nd = fetch_node(sc, k, node);
         }
         if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-        if (leaf_closest<COUNT, GEN>(sc, k, nd.y >> 2, nd.x, r, best, c) && best->l <= exit_t + EPS)
+        if (leaf_closest<COUNT, GEN, SMALL>(sc, k, nd.y >> 2, nd.x, r, best, c, mask) && best->l <= exit_t + EPS)
             return true;
         if (sp == 0) return false;
         --sp;
@@ -341,9 +348,56 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
 // KdTree::closest_ray_hit (kdtree.rs:58-64): root slab test, stack search, then the
 // unconditional renderables.  The Markstein division is used for the whole wave unless some
 // lane's origin (or the scene's splits) could underflow it.
+// Small sphere scenes (<= 32 spheres, all in LDS): an exact shortcut of the same traversal.
+// The reference returns the first leaf, front to back, whose best hit l satisfies
+// l <= exit + EPS (kdtree.rs:96).  With L* the closest valid hit over all spheres, a leaf
+// with fl(exit + EPS) < L* can never return.  Descending from entry E, where
+// fl(E + EPS) < L* holds for every value <= E, skips exactly such leaves (a near child whose
+// interval ends at or before E is not entered) and leaves every other leaf's interval, order
+// and exit untouched — so the returned sphere and distance are the reference's.  Leaves
+// only re-test spheres in the hit mask.  The instrumented (COUNT) kernel keeps the plain
+// traversal: its counters are the reference's work.
+template <bool COUNT>
+__device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
+                                              uint32_t* st, Ctr<COUNT>& c) {
+    uint32_t mask = 0;
+    float ls = __builtin_inff();
+    for (uint32_t i = 0; i < sc.n_spheres; ++i) {
+        float l;
+        const bool v = sphere_hit(fetch_sphere<false>(sc, k, i), r, &l) & !(l < HIT_MIN);
+        mask |= (v ? 1u : 0u) << i;
+        ls = v ? fminf(ls, l) : ls;
+    }
+    float root_entry, root_exit;
+    const RayAx ax = ray_axes(r);
+    if (mask && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
+        // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
+        const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
+        const float entry = fmaxf(root_entry, e);
+        bool found;
+#if RT_FASTDIV
+        const bool fast = sc.fastdiv && origin_fast_ok(r.o);
+        if (__builtin_expect(__ballot(!fast) == 0, 1))
+            found = stack_search<COUNT, false, true, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask);
+        else
+#endif
+            found = stack_search<COUNT, false, false, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask);
+        if (found) return true;
+    }
+    if (sc.has_cube) {
+        best->ref = REF_CUBE;
+        best->l = __builtin_inff();
+        return true;
+    }
+    return false;
+}
+
 template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
+#if RT_SMALL_SCENE
+    if (!GEN && !COUNT && sc.n_spheres <= 32u) return closest_small<COUNT>(sc, k, r, best, st, c);
+#endif
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
