@@ -45,11 +45,11 @@ def rank_tiles(width, height, rank, world):
     return tiles
 
 
-def roofline_bytes_per_sample(ctx, width, height, spp=16):
-    """Algorithmic bytes per sample from the device's own work counters on every 16th pixel
-    in x and y, 16 spp."""
+def roofline_bytes_per_sample(ctx, width, height, spp=16, device=False):
+    """Bytes per sample on every 16th pixel in x and y, 16 spp.  device=False:
+    the reference algorithm's work (the §8d algorithmic figure); True: the device path's."""
     tiles = [(x, y, 1, 1) for y in range(0, height, 16) for x in range(0, width, 16)]
-    c = ctx.count_work(tiles, 0, spp)
+    c = ctx.count_work(tiles, 0, spp, device=device)
     total = sum(BYTES[k] * c[k] for k in BYTES)
     trav = sum(BYTES[k] * c[k] for k in ("nodes", "leaf_refs", "sphere_tests", "tri_tests"))
     return total / c["samples"], trav / c["samples"], c
@@ -194,6 +194,7 @@ def main():
 
     if rank == 0 and not args.no_roofline:
         bps, trav_bps, counts = roofline_bytes_per_sample(ctx, w, h)
+        dev_bps, _, dev_counts = roofline_bytes_per_sample(ctx, w, h, device=True)
         avg_ms = sum(kernel_ms) / len(kernel_ms)
         achieved = bps * npix * spp_rank / (avg_ms * 1e-3) / 1e9
         spheres_only = loaded.desc.n_free_tris == 0 and loaded.desc.n_meshes == 0
@@ -209,7 +210,15 @@ def main():
                            "bytes_per_sample": round(bps, 1), "traversal_bytes_per_sample": round(trav_bps, 1),
                            "samples_per_launch": npix * spp_rank,
                            "counts_per_sample": {k: round(v / counts["samples"], 3) for k, v in counts.items()
-                                                 if k != "samples"}}
+                                                 if k != "samples"},
+                           "device_bytes_per_sample": round(dev_bps, 1),
+                           "device_frac": round(dev_bps * npix * spp_rank / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "device_counts_per_sample": {k: round(v / dev_counts["samples"], 3)
+                                                        for k, v in dev_counts.items() if k != "samples"},
+                           "note": "achieved/frac price the REFERENCE algorithm's bytes per sample (SURVEY.md "
+                                   "§8d, counted by rt_count_work); the device skips provably non-returning "
+                                   "KD leaves (closest_small), so frac can exceed 1; device_frac prices the "
+                                   "device's own logical reads; traffic is the real HBM read volume"}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(loaded, args.cpu_seconds)
     ctx.close()

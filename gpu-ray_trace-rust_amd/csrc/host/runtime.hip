@@ -473,7 +473,12 @@ extern "C" int rt_last_kernel_ms(const rt_ctx* c, float* ms) {
 
 extern "C" int rt_count_work(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
                              uint32_t sample_count, rt_work_counts* out) {
-    if (!c || !tiles || !out) return RT_ERR_INVALID_ARG;
+    return rt_count_work_ex(c, tiles, n_tiles, sample_begin, sample_count, RT_COUNT_REFERENCE, out);
+}
+
+extern "C" int rt_count_work_ex(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                                uint32_t sample_count, uint32_t mode, rt_work_counts* out) {
+    if (!c || !tiles || !out || mode > RT_COUNT_DEVICE) return RT_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     LaunchArgs a{};
     uint64_t n_out = 0;
@@ -482,6 +487,7 @@ extern "C" int rt_count_work(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, 
     a.sample_begin = sample_begin;
     a.sample_count = sample_count;
     a.counts = c->d_counts;
+    a.sc.count_device = mode == RT_COUNT_DEVICE ? 1u : 0u;
     HIPCHK(c, hipMemsetAsync(c->d_counts, 0, sizeof(DevCounts), c->stream));
     if (sample_count) HIPCHK(c, launch_trace_count(a, c->stream));
     DevCounts h{};

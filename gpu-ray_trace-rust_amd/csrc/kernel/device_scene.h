@@ -62,6 +62,7 @@ struct DevScene {
     uint32_t stack_depth;   // traversal stack entries per lane (>= max_leaf_depth, >= 1)
     uint32_t spheres_only;  // no free / mesh triangles: launch the sphere-only kernel
     uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
+    uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

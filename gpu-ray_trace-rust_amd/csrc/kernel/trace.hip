@@ -31,6 +31,9 @@
 #ifndef RT_SMALL_SCENE
 #define RT_SMALL_SCENE 1    // exact brute-force-bounded traversal for <= 32 spheres (closest_small)
 #endif
+#ifndef RT_LEAF_PMIN
+#define RT_LEAF_PMIN 1      // closest_small: a leaf holding the closest sphere needs no re-test
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
@@ -179,7 +182,20 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
 template <bool COUNT, bool GEN, bool SMALL = false>
 __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
                                              uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c,
-                                             uint32_t mask = 0) {
+                                             uint32_t mask = 0, uint32_t imin = 0, float lmin = 0.f) {
+    if (SMALL && RT_LEAF_PMIN) {
+        // If the leaf holds the globally closest sphere, that sphere is its candidate: no other
+        // leaf sphere is closer, and on a tie the lowest renderable index wins both globally and
+        // in leaf order.  Only otherwise are the leaf's masked spheres re-tested.
+        bool has_min = false;
+        for (uint32_t j = 0; j < cnt; ++j) has_min |= (sc.refs[off + j] & REF_INDEX_MASK) == imin;
+        if (has_min) {
+            best->ref = (K_SPHERE << REF_KIND_SHIFT) | imin;
+            best->l = lmin;
+            best->bu = best->bv = 0.f;
+            return true;
+        }
+    }
     bool found = false;
     for (uint32_t j = 0; j < cnt; ++j) {
         uint32_t ref = sc.refs[off + j];
@@ -305,7 +321,8 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
 template <bool COUNT, bool GEN, bool FAST, bool SMALL = false>
 __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
                                              float root_entry, float root_exit, Hit* best, uint32_t* st,
-                                             Ctr<COUNT>& c, uint32_t mask = 0) {
+                                             Ctr<COUNT>& c, uint32_t mask = 0, uint32_t imin = 0,
+                                             float lmin = 0.f) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0;
     int sp = 0;
@@ -327,7 +344,8 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
             nd = fetch_node(sc, k, node);
         }
         if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-        if (leaf_closest<COUNT, GEN, SMALL>(sc, k, nd.y >> 2, nd.x, r, best, c, mask) && best->l <= exit_t + EPS)
+        if (leaf_closest<COUNT, GEN, SMALL>(sc, k, nd.y >> 2, nd.x, r, best, c, mask, imin, lmin) &&
+            best->l <= exit_t + EPS)
             return true;
         if (sp == 0) return false;
         --sp;
@@ -360,13 +378,16 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
 template <bool COUNT>
 __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                               uint32_t* st, Ctr<COUNT>& c) {
-    uint32_t mask = 0;
+    uint32_t mask = 0, imin = 0;
     float ls = __builtin_inff();
+    if (COUNT) c.sph += sc.n_spheres;
     for (uint32_t i = 0; i < sc.n_spheres; ++i) {
         float l;
         const bool v = sphere_hit(fetch_sphere<false>(sc, k, i), r, &l) & !(l < HIT_MIN);
         mask |= (v ? 1u : 0u) << i;
-        ls = v ? fminf(ls, l) : ls;
+        const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
+        imin = better ? i : imin;
+        ls = better ? l : ls;
     }
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
@@ -378,10 +399,12 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
 #if RT_FASTDIV
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, false, true, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask);
+            found = stack_search<COUNT, false, true, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask,
+                                                           imin, ls);
         else
 #endif
-            found = stack_search<COUNT, false, false, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask);
+            found = stack_search<COUNT, false, false, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask,
+                                                            imin, ls);
         if (found) return true;
     }
     if (sc.has_cube) {
@@ -396,7 +419,7 @@ template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
 #if RT_SMALL_SCENE
-    if (!GEN && !COUNT && sc.n_spheres <= 32u) return closest_small<COUNT>(sc, k, r, best, st, c);
+    if (!GEN && (!COUNT || sc.count_device) && sc.n_spheres <= 32u) return closest_small<COUNT>(sc, k, r, best, st, c);
 #endif
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);

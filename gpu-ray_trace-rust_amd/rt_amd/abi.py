@@ -24,6 +24,7 @@ RT_DIVERT_SPEC, RT_DIVERT_DIFF, RT_DIVERT_DIFFSPEC, RT_DIVERT_DIELECTRIC = 0, 1,
 RT_ELEM_SPHERE, RT_ELEM_FREE_TRI, RT_ELEM_CUBE_MAP = 0, 1, 2
 RT_FACE_NEG_X, RT_FACE_POS_X, RT_FACE_NEG_Y, RT_FACE_POS_Y, RT_FACE_NEG_Z, RT_FACE_POS_Z = range(6)
 RT_KD_LEAF = 3
+RT_COUNT_REFERENCE, RT_COUNT_DEVICE = 0, 1
 
 f3 = C.c_float * 3
 P_f = C.POINTER(C.c_float)
@@ -127,6 +128,8 @@ EXPORTS = {
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P_f]),
     "rt_count_work": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
                                 C.POINTER(rt_work_counts)]),
+    "rt_count_work_ex": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
+                                   C.c_uint32, C.POINTER(rt_work_counts)]),
     "rt_last_error": (C.c_char_p, [C.c_void_p]),
     "rt_destroy": (C.c_int, [C.c_void_p]),
     "rt_rgba_to_u8": (C.c_int, [P_f, C.c_uint64, C.POINTER(C.c_uint8)]),

@@ -114,12 +114,14 @@ class Context:
         abi.check(self.lib, self.lib.rt_last_kernel_ms(self.ctx, C.byref(ms)), self.ctx)
         return float(ms.value)
 
-    def count_work(self, tiles=None, sample_begin: int = 0, sample_count: int = 1) -> dict:
+    def count_work(self, tiles=None, sample_begin: int = 0, sample_count: int = 1, device: bool = False) -> dict:
+        """Work counters: the reference algorithm's (default) or the device path's own."""
         tiles = tiles or self.full_tile()
         arr, n = tiles_array(tiles)
         wc = abi.rt_work_counts()
-        abi.check(self.lib, self.lib.rt_count_work(self.ctx, arr, n, int(sample_begin), int(sample_count),
-                                                   C.byref(wc)), self.ctx)
+        mode = abi.RT_COUNT_DEVICE if device else abi.RT_COUNT_REFERENCE
+        abi.check(self.lib, self.lib.rt_count_work_ex(self.ctx, arr, n, int(sample_begin), int(sample_count),
+                                                      mode, C.byref(wc)), self.ctx)
         return {k: int(getattr(wc, k)) for k, _ in abi.rt_work_counts._fields_}
 
     def close(self):

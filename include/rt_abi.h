@@ -248,9 +248,14 @@ int rt_render_device(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
 /* Device time (ms) of the last rt_render* call's trace kernel(s), from HIP events. */
 int rt_last_kernel_ms(const rt_ctx* ctx, float* ms);
 
-/* Instrumented run: same traversal, counts work instead of timing it (accumulator untouched). */
+/* Instrumented run: counts work instead of timing it (accumulator untouched).
+ * RT_COUNT_REFERENCE: the reference algorithm's work (full stack_search, kdtree.rs:66-104);
+ * RT_COUNT_DEVICE: what the device path actually does (e.g. the small-scene bound). */
+enum { RT_COUNT_REFERENCE = 0, RT_COUNT_DEVICE = 1 };
 int rt_count_work(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
                   uint64_t sample_begin, uint32_t sample_count, rt_work_counts* out);
+int rt_count_work_ex(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                     uint32_t sample_count, uint32_t mode, rt_work_counts* out);
 
 const char* rt_last_error(const rt_ctx* ctx);
 int         rt_destroy(rt_ctx* ctx);

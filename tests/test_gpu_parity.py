@@ -132,3 +132,13 @@ def test_lanes_per_pixel_bit_invariant(gpu_available, walled, monkeypatch, k, sp
         g2 = ck.render(crops, spp, 5)
     assert np.array_equal(g, ref)
     assert np.array_equal(g2, ref2)
+
+
+def test_device_work_is_a_subset_of_the_reference(ctx):
+    """The small-scene bound only skips work: same samples/segments/hits, fewer nodes."""
+    ref = ctx.count_work(CROPS[:1], 0, 4)
+    dev = ctx.count_work(CROPS[:1], 0, 4, device=True)
+    print("reference", ref, "\ndevice", dev)
+    for k in ("samples", "segments", "hits"):
+        assert dev[k] == ref[k], k
+    assert dev["nodes"] < ref["nodes"] and dev["leaf_refs"] <= ref["leaf_refs"]
