@@ -34,6 +34,9 @@
 #ifndef RT_LEAF_PMIN
 #define RT_LEAF_PMIN 1      // closest_small: a leaf holding the closest sphere needs no re-test
 #endif
+#ifndef RT_SPH_UNROLL
+#define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
@@ -381,6 +384,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
     uint32_t mask = 0, imin = 0;
     float ls = __builtin_inff();
     if (COUNT) c.sph += sc.n_spheres;
+#pragma unroll RT_SPH_UNROLL
     for (uint32_t i = 0; i < sc.n_spheres; ++i) {
         float l;
         const bool v = sphere_hit(fetch_sphere<false>(sc, k, i), r, &l) & !(l < HIT_MIN);
