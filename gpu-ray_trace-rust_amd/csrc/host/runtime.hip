@@ -28,6 +28,9 @@ struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> lev;  // start/stop pairs around each trace launch of the last call
+    uint32_t n_launch = 0;
+    float trace_ms = 0.f;
     DevScene sc{};
     std::vector<void*> allocs;
     float4* accum = nullptr;
@@ -40,6 +43,8 @@ struct rt_ctx {
     uint64_t radiance_cap = 0;    // floats
     uint64_t lane_capacity = 0;   // lanes resident at the kernel's occupancy
     uint32_t forced_k = 0;        // RT_LANES_PER_PIXEL (tests / tuning)
+    uint32_t* d_queue = nullptr;  // queue schedule item counter
+    int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
     float last_ms = 0.f;
     std::string err;
 };
@@ -106,7 +111,9 @@ static void destroy_ctx(rt_ctx* c) {
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_counts) (void)hipFree(c->d_counts);
+    if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->radiance) (void)hipFree(c->radiance);
+    for (hipEvent_t e : c->lev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -303,6 +310,11 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     hipDeviceProp_t prop;
     HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
     c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
+    if (hipMalloc(&c->d_queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
+    if (const char* e = std::getenv("RT_SCHED")) {
+        if (!std::strcmp(e, "direct")) c->sched = 1;
+        else if (!std::strcmp(e, "queue")) c->sched = 2;
+    }
     if (const char* e = std::getenv("RT_LANES_PER_PIXEL")) {
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
@@ -392,6 +404,42 @@ static int ensure_radiance(rt_ctx* c, uint64_t floats) {
 }
 
 static constexpr uint32_t SAMPLES_PER_LANE_CHUNK = 64;
+static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 30;  // 4 GiB per queue launch (of 288 GB HBM)
+
+// Schedule: the queue (persistent lanes over (pixel, sample) items, tools/variant_bench.py:
+// walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_SCHED=direct or
+// RT_LANES_PER_PIXEL asks for the direct one-lane-per-pixel schedule (kept for A/B and as the
+// tests' second path).
+static bool use_queue(const rt_ctx* c, uint64_t n_pix) {
+    (void)n_pix;
+    if (c->forced_k) return false;
+    return c->sched != 1;
+}
+
+// Records the start (begin) or stop event of the current trace launch.
+static int mark_launch(rt_ctx* c, bool begin) {
+    const size_t i = 2 * (size_t)c->n_launch + (begin ? 0 : 1);
+    while (c->lev.size() <= i) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->lev.push_back(e);
+    }
+    HIPCHK(c, hipEventRecord(c->lev[i], c->stream));
+    if (!begin) c->n_launch++;
+    return RT_OK;
+}
+
+// After the stream has drained: total time and the trace launches' share.
+static int finish_timing(rt_ctx* c) {
+    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    c->trace_ms = 0.f;
+    for (uint32_t i = 0; i < c->n_launch; ++i) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->lev[2 * i], c->lev[2 * i + 1]));
+        c->trace_ms += ms;
+    }
+    return RT_OK;
+}
 
 static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
                        uint32_t sample_count, float4* dev_out) {
@@ -401,11 +449,43 @@ static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64
     int st = prepare_tiles(c, tiles, n_tiles, K, &a, &n_out);
     if (st) return st;
     a.out = dev_out;
+    c->n_launch = 0;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if (K == 1) {
+    if (use_queue(c, n_out)) {
+        uint64_t chunk = QUEUE_RADIANCE_FLOATS / (3 * n_out);
+        if (chunk < 1) chunk = 1;
+        if (chunk > sample_count) chunk = sample_count ? sample_count : 1;
+        const uint64_t lanes = c->lane_capacity;
+        // the counter overshoots n_items by at most one grab (<= 1024 = 16 x 64) per wave
+        if ((uint64_t)n_out * chunk + lanes * 16 >= (1ull << 32)) chunk = ((1ull << 32) - lanes * 16 - 1) / n_out;
+        if (chunk < 1) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels for one launch");
+        if (sample_count > chunk) {  // equal launches: ceil(count / n) samples each
+            const uint64_t n = (sample_count + chunk - 1) / chunk;
+            chunk = (sample_count + n - 1) / n;
+        }
+        if ((st = ensure_radiance(c, 3 * n_out * chunk))) return st;
+        a.radiance = c->radiance;
+        a.queue = c->d_queue;
+        uint32_t done = 0;
+        do {
+            a.sample_begin = sample_begin + done;
+            a.sample_count = (uint32_t)(sample_count - done < chunk ? sample_count - done : chunk);
+            a.n_items = (uint32_t)(n_out * a.sample_count);
+            if (a.sample_count) {
+                HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), c->stream));
+                if ((st = mark_launch(c, true))) return st;
+                HIPCHK(c, launch_trace_queue(a, (uint32_t)(lanes / BLOCK), c->stream));
+                if ((st = mark_launch(c, false))) return st;
+            }
+            HIPCHK(c, launch_fold(a, c->stream));
+            done += a.sample_count;
+        } while (done < sample_count);
+    } else if (K == 1) {
         a.sample_begin = sample_begin;
         a.sample_count = sample_count;
+        if ((st = mark_launch(c, true))) return st;
         HIPCHK(c, launch_trace(a, c->stream));  // count 0 still (re)writes the accumulators
+        if ((st = mark_launch(c, false))) return st;
     } else {
         const uint32_t chunk = sample_count < SAMPLES_PER_LANE_CHUNK * K ? sample_count : SAMPLES_PER_LANE_CHUNK * K;
         if ((st = ensure_radiance(c, 3 * n_out * (chunk ? chunk : 1)))) return st;
@@ -414,7 +494,11 @@ static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64
         do {
             a.sample_begin = sample_begin + done;
             a.sample_count = sample_count - done < chunk ? sample_count - done : chunk;
-            if (a.sample_count) HIPCHK(c, launch_trace(a, c->stream));
+            if (a.sample_count) {
+                if ((st = mark_launch(c, true))) return st;
+                HIPCHK(c, launch_trace(a, c->stream));
+                if ((st = mark_launch(c, false))) return st;
+            }
             HIPCHK(c, launch_fold(a, c->stream));
             done += a.sample_count;
         } while (done < sample_count);
@@ -450,8 +534,7 @@ extern "C" int rt_render(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
     if (out_rgba)
         HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    return RT_OK;
+    return finish_timing(c);
 }
 
 extern "C" int rt_render_device(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles,
@@ -461,13 +544,21 @@ extern "C" int rt_render_device(rt_ctx* c, const rt_tile* tiles, uint32_t n_tile
     int st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, reinterpret_cast<float4*>(out_dev));
     if (st) return st;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    return RT_OK;
+    return finish_timing(c);
 }
 
 extern "C" int rt_last_kernel_ms(const rt_ctx* c, float* ms) {
     if (!c || !ms) return RT_ERR_INVALID_ARG;
     *ms = c->last_ms;
+    return RT_OK;
+}
+
+extern "C" int rt_last_launch_stats(const rt_ctx* c, rt_launch_stats* out) {
+    if (!c || !out) return RT_ERR_INVALID_ARG;
+    out->render_ms = c->last_ms;
+    out->trace_ms = c->trace_ms;
+    out->n_trace_launches = c->n_launch;
+    out->_pad0 = 0;
     return RT_OK;
 }
 

@@ -125,11 +125,17 @@ struct LaunchArgs {
     uint32_t lanes_per_pixel;
     uint32_t n_pix;         // pixels of the launch (tiles concatenated)
     float* radiance;
+    // Queue schedule (launch_trace_queue): persistent lanes take (pixel, sample) items
+    // item = j * n_pix + o (sample j of the launch, output pixel o) from *queue in wave-sized
+    // grabs, trace them into `radiance` and fold_kernel folds them in sample order.
+    uint32_t* queue;
+    uint32_t n_items;       // n_pix * sample_count
 };
 
 // Launch wrappers (trace.hip).
 hipError_t launch_trace(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_fold(const LaunchArgs& a, hipStream_t s);
+hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s);
 
 }  // namespace rtd

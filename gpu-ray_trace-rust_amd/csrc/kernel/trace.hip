@@ -790,6 +790,115 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     }
 }
 
+// Tile holding launch pixel o (tiles are concatenated in out_off order).
+__device__ __forceinline__ uint32_t tile_of(const LaunchArgs& a, uint32_t o) {
+    uint32_t lo = 0, hi = a.n_tiles - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (a.tiles[mid].out_off <= o) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Queue schedule: the grid is sized to the resident lanes, and every lane keeps tracing
+// (pixel, sample) items until the launch's items are exhausted, so a wave is never held back
+// by its slowest pixel (mesh scenes, where a sky pixel costs a fraction of an airplane pixel).
+// A wave claims a run of consecutive items per atomic and hands them to its idle lanes in lane
+// order; consecutive items are neighbouring pixels of one sample.  The run length adapts to
+// what is left — about remaining / (RT_QDIV * waves), in multiples of 64, from 64 to RT_QMAX —
+// so the single counter is hit rarely while most items remain (a cheap scene otherwise
+// saturates it) and balance is fine-grained at the end of the launch.  Each item's radiance goes
+// to radiance[j][o]; fold_kernel then applies the running mean in sample order, so the image is
+// the direct schedule's, bit for bit.
+#ifndef RT_QDIV
+#define RT_QDIV 16
+#endif
+#ifndef RT_QMAX
+#define RT_QMAX 1024
+#endif
+__device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_waves) {
+    uint32_t g = remaining / (RT_QDIV * n_waves);
+    g &= ~63u;
+    return g < 64u ? 64u : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
+}
+
+template <bool GEN>
+#if RT_MIN_WAVES > 0
+__global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
+#else
+__global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
+#endif
+    extern __shared__ uint32_t dyn_lds[];
+    const DevScene& sc = a.sc;
+    Cache k{0, 0};
+#if RT_LDS_NODES > 0
+    k.n_nodes = sc.n_nodes < (uint32_t)RT_LDS_NODES ? sc.n_nodes : (uint32_t)RT_LDS_NODES;
+    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
+#endif
+#if RT_LDS_SPHERES > 0
+    k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+#endif
+#if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
+    __syncthreads();
+#endif
+    uint32_t* st = dyn_lds + threadIdx.x;
+    Ctr<false> c;
+    const uint32_t lane = __lane_id();
+    uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
+    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    uint32_t grab = grab_size(a.n_items, n_waves);
+    bool have = false, done = false;
+    uint32_t slot = 0;                // radiance index of the lane's item
+    Path p;
+    for (;;) {
+        const uint64_t need = __ballot(!have && !done);
+        if (need) {
+            const uint32_t n = (uint32_t)__popcll(need);
+            const uint32_t left = pool_end - pool;
+            uint32_t base = pool_end;
+            if (left < n) {
+                uint32_t b0 = 0;
+                const uint32_t first = (uint32_t)__ffsll((unsigned long long)need) - 1u;
+                if (lane == first) b0 = atomicAdd(a.queue, grab);
+                base = __builtin_amdgcn_readfirstlane(__shfl(b0, first));
+            }
+            if (!have && !done) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint32_t item = r < left ? pool + r : base + (r - left);
+                if (item < a.n_items) {
+                    const uint32_t j = item / a.n_pix, o = item - j * a.n_pix;
+                    const DevTile tl = a.tiles[tile_of(a, o)];
+                    const uint32_t lo = o - tl.out_off;
+                    const int x = (int)(tl.x0 + lo % tl.w), y = (int)(tl.y0 + lo / tl.w);
+                    start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
+                    slot = item;
+                    have = true;
+                } else {
+                    done = true;
+                }
+            }
+            if (left < n) {
+                pool = base + (n - left);
+                pool_end = base + grab;
+                grab = grab_size(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+            } else {
+                pool += n;
+            }
+        }
+        if (__ballot(have) == 0) break;
+        if (have && segment<false, GEN>(sc, k, p, st, c)) {
+            float* r = a.radiance + 3 * (size_t)slot;
+            r[0] = p.L.x;
+            r[1] = p.L.y;
+            r[2] = p.L.z;
+            have = false;
+        }
+    }
+}
+
 // Running mean over the traced chunk, in sample order (draw_scene.rs:81-83): one lane per
 // launch pixel; reads are coalesced across lanes ([sample][pixel] layout).
 __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
@@ -827,6 +936,13 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((trace_kernel<false, false>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else
         hipLaunchKernelGGL((trace_kernel<false, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    return hipGetLastError();
+}
+hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
+    if (a.sc.spheres_only)
+        hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    else
+        hipLaunchKernelGGL((queue_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s) {

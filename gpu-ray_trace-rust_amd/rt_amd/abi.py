@@ -106,6 +106,11 @@ class rt_kd_tree(C.Structure):
                 ("nodes", C.POINTER(rt_kd_node)), ("refs", P_u32), ("unconditional", P_u32)]
 
 
+class rt_launch_stats(C.Structure):
+    _fields_ = [("render_ms", C.c_float), ("trace_ms", C.c_float), ("n_trace_launches", C.c_uint32),
+                ("_pad0", C.c_uint32)]
+
+
 class rt_work_counts(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "segments", "nodes", "leaf_refs", "sphere_tests",
                                            "tri_tests", "hits", "mesh_hits")]
@@ -126,6 +131,7 @@ EXPORTS = {
     "rt_render_device": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
                                    C.c_void_p]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P_f]),
+    "rt_last_launch_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_launch_stats)]),
     "rt_count_work": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
                                 C.POINTER(rt_work_counts)]),
     "rt_count_work_ex": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,

@@ -114,6 +114,13 @@ class Context:
         abi.check(self.lib, self.lib.rt_last_kernel_ms(self.ctx, C.byref(ms)), self.ctx)
         return float(ms.value)
 
+    def launch_stats(self) -> dict:
+        """{render_ms, trace_ms, n_trace_launches} of the last render call."""
+        st = abi.rt_launch_stats()
+        abi.check(self.lib, self.lib.rt_last_launch_stats(self.ctx, C.byref(st)), self.ctx)
+        return {"render_ms": float(st.render_ms), "trace_ms": float(st.trace_ms),
+                "n_trace_launches": int(st.n_trace_launches)}
+
     def count_work(self, tiles=None, sample_begin: int = 0, sample_count: int = 1, device: bool = False) -> dict:
         """Work counters: the reference algorithm's (default) or the device path's own."""
         tiles = tiles or self.full_tile()

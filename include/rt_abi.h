@@ -245,8 +245,20 @@ int rt_render(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
 int rt_render_device(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
                      uint64_t sample_begin, uint32_t sample_count, float* out_rgba_device);
 
-/* Device time (ms) of the last rt_render* call's trace kernel(s), from HIP events. */
+/* Device time (ms) of the last rt_render* call, first launch to last (trace + fold), from HIP
+ * events. */
 int rt_last_kernel_ms(const rt_ctx* ctx, float* ms);
+
+/* Per-launch breakdown of the last rt_render* call: the trace kernel launches alone (HIP events
+ * around each one), their count, and the whole call.  Samples per trace launch follow from the
+ * call's pixels x samples / n_trace_launches. */
+typedef struct rt_launch_stats {
+    float render_ms;            /* same as rt_last_kernel_ms */
+    float trace_ms;             /* sum over the trace kernel launches */
+    uint32_t n_trace_launches;
+    uint32_t _pad0;
+} rt_launch_stats;
+int rt_last_launch_stats(const rt_ctx* ctx, rt_launch_stats* out);
 
 /* Instrumented run: counts work instead of timing it (accumulator untouched).
  * RT_COUNT_REFERENCE: the reference algorithm's work (full stack_search, kdtree.rs:66-104);

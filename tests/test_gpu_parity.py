@@ -142,3 +142,24 @@ def test_device_work_is_a_subset_of_the_reference(ctx):
     for k in ("samples", "segments", "hits"):
         assert dev[k] == ref[k], k
     assert dev["nodes"] < ref["nodes"] and dev["leaf_refs"] <= ref["leaf_refs"]
+
+
+@pytest.mark.parametrize("scene_name,spp", [("walled", 37), ("walled", 5), ("biplane", 3), ("spaceship_r1", 2)])
+def test_queue_schedule_bit_invariant(gpu_available, monkeypatch, scene_name, spp):
+    """Queue schedule (persistent lanes over (pixel, sample) items + in-order fold) == direct
+    one-lane-per-pixel schedule, bit for bit, over several tiles and a second sample range."""
+    from rt_amd import render
+
+    sc = load_scene(scene_name)
+    w, h = sc.info.width, sc.info.height
+    tiles = [(w // 2 - 40, h // 2 - 20, 80, 40), (0, 0, 7, 3), (w - 33, h - 9, 33, 9)]
+    monkeypatch.setenv("RT_SCHED", "direct")
+    with render.Context(sc) as c1:
+        ref = c1.render(tiles, 0, spp)
+        ref2 = c1.render(tiles, spp, 4)
+    monkeypatch.setenv("RT_SCHED", "queue")
+    with render.Context(sc) as cq:
+        g = cq.render(tiles, 0, spp)
+        g2 = cq.render(tiles, spp, 4)
+    assert np.array_equal(g, ref)
+    assert np.array_equal(g2, ref2)

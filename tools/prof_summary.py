@@ -10,12 +10,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(path, kernel="trace_kernel"):
+def counters(path, kernels=("queue_kernel", "trace_kernel")):
     rows = list(csv.DictReader(open(path)))
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for r in rows:
-        if kernel in r["Kernel_Name"] and "<true" not in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if any(n in k for n in kernels) and "trace_kernel<true" not in k:
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"]
     return per, names
@@ -65,11 +66,10 @@ def main(tag):
                     if l.startswith("{"):
                         cfg = json.loads(l)
             scene = cfg.get("metric", "").split(" on ")[-1].replace(".yml", "") if cfg else None
-            spp = cfg.get("config", {}).get("spp_per_step")
-            npix = cfg.get("config", {}).get("pixels")
-            json.dump({"scene": scene, "samples_per_launch": (spp or 0) * (npix or 0) * cfg.get("n_gpus", 1),
+            spl = cfg.get("launch", {}).get("samples_per_launch", 0)
+            json.dump({"scene": scene, "samples_per_launch": spl,
                        "hbm_read_bytes_per_launch": int(2 * d["FETCH_SIZE"] * 1024),
-                       "note": "rocprofv3 --pmc FETCH_SIZE, own pass, last trace_kernel dispatch, x2 per "
+                       "note": "rocprofv3 --pmc FETCH_SIZE, own pass, last trace dispatch, x2 per "
                                "MI355X_MICROARCH.md HBM section"},
                       open(os.path.join(dst, f"{tag}_fetch.json"), "w"), indent=1)
         if "SQ_WAVE_CYCLES" in d:

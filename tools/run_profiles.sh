@@ -6,7 +6,7 @@
 # Usage: tools/run_profiles.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r1}; shift
-ARGS=${@:---spp-per-step 64 --steps 3 --warmup 1}
+ARGS=${@:---steps 2 --warmup 1}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
