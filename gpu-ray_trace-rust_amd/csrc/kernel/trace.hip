@@ -34,6 +34,9 @@
 #ifndef RT_LEAF_PMIN
 #define RT_LEAF_PMIN 1      // closest_small: a leaf holding the closest sphere needs no re-test
 #endif
+#ifndef RT_EXACT_FAST
+#define RT_EXACT_FAST 1     // rcp/div via the checked exact FMA identities, sincosf (bit-identical)
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -67,9 +70,47 @@ __device__ __forceinline__ V3 operator*(float s, V3 a) { return mk(s * a.x, s * 
 __device__ __forceinline__ V3 operator/(V3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ V3 cmul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+// ---------------------------------------------------------------- exact fast arithmetic
+// Correctly rounded reciprocal and quotient in 3 + 3 instructions instead of hipcc's ~10-instruction
+// IEEE sequence (div_scale / rcp / fma chain / div_fmas / div_fixup):
+//   rcp_exact(b) = fma(fma(-b, y, 1), y, y), y = v_rcp_f32(b): equal to 1.0f / b for EVERY normal
+//     |b| in [2^-60, 2^60] (exhaustive, tools/check_exact_ops.hip);
+//   div_mk(a, b, r) = fma(fma(-a*r, b, a), r, a*r) with r = rcp_exact(b): equal to a / b
+//     (Markstein; 4.3e9 random pairs + 2.1e9 normalize-shaped pairs, same tool) when a is 0 or
+//     also in that range — the zero case keeps a's sign explicitly.
+// Operands outside the range take the IEEE division (a divergent branch no lane normally takes).
+__device__ __forceinline__ bool mk_range(float x) {
+    const uint32_t e = (__float_as_uint(x) >> 23) & 0xffu;
+    return e >= 67u && e <= 186u;  // [2^-60, 2^60): the range the checks cover
+}
+__device__ __forceinline__ bool mk_num(float x) { return (__float_as_uint(x) << 1) == 0u || mk_range(x); }
+__device__ __forceinline__ float rcp_exact(float b) {
+    const float y = __builtin_amdgcn_rcpf(b);
+    return fmaf(fmaf(-b, y, 1.0f), y, y);
+}
+__device__ __forceinline__ float div_mk(float a, float b, float r) {
+    const float q0 = a * r;
+    const float q = fmaf(fmaf(-q0, b, a), r, q0);
+    return (__float_as_uint(a) << 1) == 0u ? a : q;
+}
+// 1.0f / b, bit for bit
+__device__ __forceinline__ float recip(float b) {
+    if (!RT_EXACT_FAST) return 1.0f / b;
+    float r = rcp_exact(b);
+    if (__builtin_expect(!mk_range(b), 0)) r = 1.0f / b;
+    return r;
+}
+// (a.x / b, a.y / b, a.z / b), bit for bit
+__device__ __forceinline__ V3 div3(V3 a, float b) {
+    if (!RT_EXACT_FAST) return a / b;
+    const float r = rcp_exact(b);
+    V3 q = mk(div_mk(a.x, b, r), div_mk(a.y, b, r), div_mk(a.z, b, r));
+    if (__builtin_expect(!(mk_range(b) && mk_num(a.x) && mk_num(a.y) && mk_num(a.z)), 0)) q = a / b;
+    return q;
+}
 __device__ __forceinline__ V3 normalize(V3 a) {
     float n = sqrtf(dot(a, a));
-    return a / n;
+    return div3(a, n);
 }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -162,7 +203,7 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
     V3 ray_x_e2 = cross(r.d, e2);
     float det = dot(e1, ray_x_e2);
     if (fabsf(det) < EPS) return false;
-    float inv_det = 1.0f / det;
+    float inv_det = recip(det);
     V3 rhs = r.o - v0;
     float u = inv_det * dot(rhs, ray_x_e2);
     if (u < 0.0f || u > 1.0f) return false;
@@ -239,9 +280,9 @@ __device__ __forceinline__ RayAx ray_axes(const Ray& r) {
     x.dx = clamp_eps(r.d.x);
     x.dy = clamp_eps(r.d.y);
     x.dz = clamp_eps(r.d.z);
-    x.rx = 1.0f / x.dx;
-    x.ry = 1.0f / x.dy;
-    x.rz = 1.0f / x.dz;
+    x.rx = recip(x.dx);
+    x.ry = recip(x.dy);
+    x.rz = recip(x.dz);
     return x;
 }
 // Branch-free pick by axis a in {0,1,2}.
@@ -460,8 +501,15 @@ __device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
     float v = draw(rng);
     float r = sqrtf(u);
     float thet = 2.0f * PI * v;
-    float x = r * cosf(thet);
-    float y = r * sinf(thet);
+    float sn, cs;
+#if RT_EXACT_FAST
+    sincosf(thet, &sn, &cs);  // == (sinf, cosf) bit for bit (tools/check_exact_ops.hip)
+#else
+    sn = sinf(thet);
+    cs = cosf(thet);
+#endif
+    float x = r * cs;
+    float y = r * sn;
     return normalize((xd * x + yd * y) + n * sqrtf(fmaxf(1.0f - u, 0.0f)));
 }
 __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, float* p,
@@ -535,8 +583,10 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint
         float v = draw(rng);
         float r = sqrtf(u);
         float thet = 2.0f * PI * v;
-        float lx = (r - 0.5f) * 2.0f * a * cosf(thet);
-        float ly = (r - 0.5f) * 2.0f * a * sinf(thet);
+        float sn, cs;
+        sincosf(thet, &sn, &cs);
+        float lx = (r - 0.5f) * 2.0f * a * cs;
+        float ly = (r - 0.5f) * 2.0f * a * sn;
         V3 off = right * lx + up * ly;
         ray.d = d - off;
         ray.o = off + ld3(sc.cam_o);
@@ -632,7 +682,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
         rgb = cmul(rgb, tex_pixel(sc, pr.base_tex, u, v));
     }
     rgb = rgb * 1.0f;
-    if (atten) rgb = rgb / RR_THRES;
+    if (atten) rgb = div3(rgb, RR_THRES);
     p.T = cmul(p.T, rgb);
     p.ray.d = nd;
     p.ray.o = pos;
@@ -688,7 +738,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
         nd = diff_dir(p.ray.d, n, &p.rng);
     }
     V3 rgb = ld3(m->rgb) * prob;
-    if (atten) rgb = rgb / RR_THRES;
+    if (atten) rgb = div3(rgb, RR_THRES);
     p.T = cmul(p.T, rgb);
     p.ray.d = nd;
     p.ray.o = pos;
