@@ -1,5 +1,5 @@
 """Device path vs the CPU oracle on the other benchmark scenes: triangles.yml (free triangles,
-thin lens, cube map), biplane.yml and spaceship_r1.yml (glTF meshes: normal maps, base colour
+thin lens, cube map), a380.yml (synthetic stand-in geometry), biplane.yml and spaceship_r1.yml (glTF meshes: normal maps, base colour
 and metallic-roughness textures, tangents, Schlick/roughness sampling, cube-map sky)."""
 import numpy as np
 import pytest
@@ -13,8 +13,9 @@ CROPS = {
     "triangles": [(560, 260, 64, 32), (600, 500, 32, 32), (100, 100, 32, 16)],
     "biplane": [(600, 400, 32, 32), (450, 300, 32, 32), (600, 300, 32, 16)],
     "spaceship_r1": [(450, 200, 32, 32), (600, 300, 32, 32), (750, 400, 32, 16)],
+    "a380": [(350, 400, 32, 32), (450, 275, 32, 32), (750, 425, 32, 16)],
 }
-SPP = {"triangles": 16, "biplane": 8, "spaceship_r1": 8}
+SPP = {"triangles": 16, "biplane": 8, "spaceship_r1": 8, "a380": 4}
 
 
 @pytest.fixture(scope="module", params=sorted(CROPS))

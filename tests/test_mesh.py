@@ -9,7 +9,7 @@ import pytest
 from conftest import load_scene
 
 
-@pytest.fixture(scope="module", params=["biplane", "spaceship_r1"])
+@pytest.fixture(scope="module", params=["biplane", "spaceship_r1", "a380"])
 def mesh_scene(request):
     return request.param, load_scene(request.param)
 
@@ -17,8 +17,15 @@ def mesh_scene(request):
 def test_scene_shapes(mesh_scene):
     name, sc = mesh_scene
     tris = sum(m.n_tris for m in sc.scene.meshes)
-    # biplane 7,316 triangles; spaceship 2,097
-    assert tris == {"biplane": 7316, "spaceship_r1": 2097}[name]
+    # biplane 7,316 triangles; spaceship 2,097; a380 127,749 (synthetic stand-in
+    # with the real glTF's 32 primitives and counts, tools/make_a380_standin.py)
+    assert tris == {"biplane": 7316, "spaceship_r1": 2097, "a380": 127749}[name]
+    if name == "a380":
+        prims = [p for m in sc.scene.meshes for p in m.prims]
+        assert len(prims) == 32 and sum(len(p.poses) for p in prims) == 312143
+        # material 8 of the glTF has no baseColorTexture; no primitive has a normal map
+        assert sum(p.base_tex >= 0 for p in prims) == 31 and all(p.normal_tex < 0 for p in prims)
+        return
     p = sc.scene.meshes[0].prims[0]
     assert p.normal_tex >= 0 and p.base_tex >= 0 and p.tangents is not None
     # spaceship: metallicRoughness image is missing from the snapshot -> declared fallback
@@ -34,7 +41,7 @@ def test_kd_equal_to_oracle(mesh_scene, oracle):
     orows, orefs, ob = oracle.kd_dump(sc.desc, 17)
     assert np.array_equal(rows, orows) and np.array_equal(refs, orefs) and np.array_equal(ob, kd.bounds)
     # SURVEY.md §8a row 6 node counts (reachable nodes; the array adds block padding)
-    assert len(rows) == {"biplane": 467349, "spaceship_r1": 359075}[name]
+    assert len(rows) == {"biplane": 467349, "spaceship_r1": 359075, "a380": 505635}[name]
 
 
 def test_normal_transforms_equal_to_oracle(mesh_scene, oracle, rtlib):
