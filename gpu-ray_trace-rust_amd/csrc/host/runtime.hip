@@ -159,7 +159,9 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         uint32_t ri = tree->refs[i];
         if (ri >= rs.size() || !rs[ri].has_aabb) return set_err(c, RT_ERR_INVALID_ARG, "bad leaf ref");
         uint32_t kind = rs[ri].kind == RT_KIND_SPHERE ? K_SPHERE : (rs[ri].kind == RT_KIND_FREE_TRI ? K_FREE_TRI : K_MESH_TRI);
-        refs[i] = (kind << REF_KIND_SHIFT) | rs[ri].index;
+        const uint32_t base = kind == K_SPHERE ? 0u : (kind == K_FREE_TRI ? scene->n_spheres
+                                                                          : scene->n_spheres + scene->n_free_tris);
+        refs[i] = (kind << REF_KIND_SHIFT) | (base + rs[ri].index);  // pool index (DevScene::prim4)
     }
     std::vector<uint2> nodes(tree->n_nodes);
     for (uint32_t i = 0; i < tree->n_nodes; ++i) nodes[i] = make_uint2(tree->nodes[i].a, tree->nodes[i].b);
@@ -251,12 +253,22 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if ((st = upload(c, refs, &d.refs))) return st;
     if ((st = upload(c, sph, &d.sph))) return st;
     if ((st = upload(c, sph_mat, &d.sph_mat))) return st;
-    if ((st = upload(c, ftri, &d.ftri))) return st;
+    {   // the leaf-test pool: spheres, free triangles, mesh triangles, 3 float4 each
+        const size_t n_mesh = mf.tris.size();
+        if ((uint64_t)scene->n_spheres + scene->n_free_tris + n_mesh >= (1ull << 30))
+            return set_err(c, RT_ERR_INVALID_ARG, "too many primitives");
+        std::vector<float4> pool(3 * ((size_t)scene->n_spheres + scene->n_free_tris + n_mesh), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (uint32_t i = 0; i < scene->n_spheres; ++i) pool[3 * (size_t)i] = sph[i];
+        std::memcpy(pool.data() + 3 * (size_t)scene->n_spheres, ftri.data(), ftri.size() * sizeof(float4));
+        if (n_mesh) std::memcpy(pool.data() + 3 * ((size_t)scene->n_spheres + scene->n_free_tris), mf.verts.data(), 3 * n_mesh * sizeof(float4));
+        if ((st = upload(c, pool, &d.prim4))) return st;
+        d.pool_ftri = scene->n_spheres;
+        d.pool_mesh = scene->n_spheres + scene->n_free_tris;
+    }
     if ((st = upload(c, ftri_n, &d.ftri_n))) return st;
     if ((st = upload(c, ftri_mat, &d.ftri_mat))) return st;
     if ((st = upload(c, texels, &d.texels))) return st;
     if ((st = upload(c, texs, &d.tex))) return st;
-    if ((st = upload(c, as_f4(mf.verts), &d.mtri_v))) return st;
     if ((st = upload(c, mtri, &d.mtri))) return st;
     if ((st = upload(c, prims, &d.prims))) return st;
     if ((st = upload(c, as_f4(mf.norms), &d.vnorm))) return st;

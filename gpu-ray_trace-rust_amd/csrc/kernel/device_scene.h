@@ -69,11 +69,14 @@ struct DevScene {
     const DevMat* sph_mat;
     uint32_t n_spheres;
     // free triangles
-    const float4* ftri;     // 3 per triangle: v0, v1, v2 (w unused)
+    // Leaf-testable primitives, 3 float4 each, indexed by a device ref's index:
+    // [spheres: {c, r}, 0, 0][free triangles: v0, v1, v2][mesh triangles: v0, v1, v2].
+    // A ref's index is its pool position; per-kind arrays below take index - pool_<kind>.
+    const float4* prim4;
+    uint32_t pool_ftri, pool_mesh;
     const float4* ftri_n;   // uniform normal
     const DevMat* ftri_mat;
     // mesh triangles (src/elements/mesh)
-    const float4* mtri_v;   // 3 per triangle: pre-gathered positions
     const DevMeshTri* mtri;
     const DevPrim* prims;
     const float4* vnorm;    // per global vertex

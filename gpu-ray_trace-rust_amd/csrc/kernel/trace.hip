@@ -37,6 +37,12 @@
 #ifndef RT_EXACT_FAST
 #define RT_EXACT_FAST 1     // rcp/div via the checked exact FMA identities, sincosf (bit-identical)
 #endif
+#ifndef RT_TRI_BF
+#define RT_TRI_BF 0         // branch-free Moller-Trumbore (same operations, predicates combined): no gain
+#endif
+#ifndef RT_LEAF2
+#define RT_LEAF2 2          // general leaves: refs per step, all their loads issued first (1: plain loop)
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -218,11 +224,80 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
     return true;
 }
 
+// The same test without early exits: every quantity is computed with the reference's operations
+// and order, and the four rejections are combined into one predicate (NaN compares exactly as
+// the early exits do).  inv_det is exact for |det| in [EPS, 2^60) (rcp_exact); a rejected det's
+// reciprocal is never used.
+__device__ __forceinline__ bool tri_hit_bf(V3 v0, V3 v1, V3 v2, const Ray& r, float* l, float* bu,
+                                           float* bv) {
+    const V3 e1 = v1 - v0;
+    const V3 e2 = v2 - v0;
+    const V3 ray_x_e2 = cross(r.d, e2);
+    const float det = dot(e1, ray_x_e2);
+    float inv_det = RT_EXACT_FAST ? rcp_exact(det) : 1.0f / det;
+    if (RT_EXACT_FAST && __builtin_expect(fabsf(det) >= 0x1p60f, 0)) inv_det = 1.0f / det;
+    const V3 rhs = r.o - v0;
+    const float u = inv_det * dot(rhs, ray_x_e2);
+    const V3 rhs_x_e1 = cross(rhs, e1);
+    const float v = inv_det * dot(r.d, rhs_x_e1);
+    const float t = inv_det * dot(e2, rhs_x_e1);
+    *l = t;
+    *bu = u;
+    *bv = v;
+    return !(fabsf(det) < EPS) & !(u < 0.0f || u > 1.0f) & !(v < 0.0f || (u + v) > 1.0f) & !(t < EPS);
+}
+
 // Aabb::get_entry_exit (aabb.rs:22-62)
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
 // hits not shorter than 20*EPS.
 // SMALL: `mask` has bit i set iff sphere i has a valid hit (closest_small); other spheres
 // cannot be the leaf's candidate and are not re-tested.
+// Device data of a leaf ref: a sphere's float4 {c, r} or a triangle's three vertices.
+__device__ __forceinline__ const float4* prim_data(const DevScene& sc, uint32_t ref) {
+    const uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
+    (void)kind;
+    return sc.prim4 + 3 * (size_t)idx;
+}
+// One ref of a general leaf with its primitive's data (loaded ahead of the test).
+struct LeafSlot {
+    uint32_t ref;
+    float4 a0, a1, a2;
+    __device__ __forceinline__ void load(const DevScene& sc) {
+        const float4* p = prim_data(sc, ref);
+        a0 = p[0];
+        a1 = p[1];
+        a2 = p[2];
+    }
+};
+// One ref of closest_ray_hit (closest_hit.rs:6-30) in the general kernel.
+template <bool COUNT>
+__device__ __forceinline__ void leaf_step(const LeafSlot& sl, const Ray& r, Hit* best, bool& found,
+                                          Ctr<COUNT>& c) {
+    const uint32_t ref = sl.ref;
+    const float4 a0 = sl.a0, a1 = sl.a1, a2 = sl.a2;
+    float l = 0.f, bu = 0.f, bv = 0.f;
+    bool h;
+    if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) {
+        if (COUNT) c.sph++;
+        h = sphere_hit(a0, r, &l);
+    } else {
+        if (COUNT) c.tri++;
+#if RT_TRI_BF
+        h = tri_hit_bf(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
+#else
+        h = tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
+#endif
+    }
+    const bool above = !raylen_less(l, HIT_MIN);  // RayLen order: NaN sorts above everything
+    const bool closer = raylen_less(l, best->l);
+    const bool take = h & above & (!found | closer);
+    best->ref = take ? ref : best->ref;
+    best->l = take ? l : best->l;
+    best->bu = take ? bu : best->bu;
+    best->bv = take ? bv : best->bv;
+    found = found || take;
+}
+
 template <bool COUNT, bool GEN, bool SMALL = false>
 __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
                                              uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c,
@@ -241,6 +316,33 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
         }
     }
     bool found = false;
+#if RT_LEAF2
+    if (GEN && !SMALL) {
+        // RT_LEAF2 refs per step: every ref and every primitive's data of the step is loaded
+        // before any is tested, so a lane keeps RT_LEAF2 dependent load chains in flight.  A
+        // sphere reads its float4 and the two padding float4s after it (the array is padded);
+        // steps past the leaf's end re-read its last ref and skip the test.
+        constexpr uint32_t N = RT_LEAF2 > 1 ? RT_LEAF2 : 1;
+        static_assert(N <= 4, "RT_LEAF2 <= 4");
+        for (uint32_t j = 0; j < cnt; j += N) {
+            const uint32_t last = cnt - 1;
+            LeafSlot s0, s1, s2, s3;
+            s0.ref = sc.refs[off + j];
+            if constexpr (N > 1) s1.ref = sc.refs[off + (j + 1 < cnt ? j + 1 : last)];
+            if constexpr (N > 2) s2.ref = sc.refs[off + (j + 2 < cnt ? j + 2 : last)];
+            if constexpr (N > 3) s3.ref = sc.refs[off + (j + 3 < cnt ? j + 3 : last)];
+            s0.load(sc);
+            if constexpr (N > 1) s1.load(sc);
+            if constexpr (N > 2) s2.load(sc);
+            if constexpr (N > 3) s3.load(sc);
+            leaf_step<COUNT>(s0, r, best, found, c);
+            if constexpr (N > 1) if (j + 1 < cnt) leaf_step<COUNT>(s1, r, best, found, c);
+            if constexpr (N > 2) if (j + 2 < cnt) leaf_step<COUNT>(s2, r, best, found, c);
+            if constexpr (N > 3) if (j + 3 < cnt) leaf_step<COUNT>(s3, r, best, found, c);
+        }
+        return found;
+    }
+#endif
     for (uint32_t j = 0; j < cnt; ++j) {
         uint32_t ref = sc.refs[off + j];
         uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
@@ -252,7 +354,7 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
             h = sphere_hit(fetch_sphere<GEN>(sc, k, idx), r, &l);
         } else {
             if (COUNT) c.tri++;
-            const float4* v = (kind == K_FREE_TRI ? sc.ftri : sc.mtri_v) + 3 * (size_t)idx;
+            const float4* v = sc.prim4 + 3 * (size_t)idx;
             h = tri_hit(xyz(v[0]), xyz(v[1]), xyz(v[2]), r, &l, &bu, &bv);
         }
         // spheres never produce a NaN length: plain compares; triangles keep RayLen's order
@@ -704,7 +806,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
         return true;
     }
     const uint32_t kind = h.ref >> REF_KIND_SHIFT, idx = h.ref & REF_INDEX_MASK;
-    if (GEN && kind == K_MESH_TRI) return mesh_segment<COUNT>(sc, h, idx, p, c);
+    if (GEN && kind == K_MESH_TRI) return mesh_segment<COUNT>(sc, h, idx - sc.pool_mesh, p, c);
     V3 n, pos;
     const DevMat* m;
     if (!GEN || kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
@@ -714,9 +816,9 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
         pos = perfect + n * EPS;
         m = sc.sph_mat + idx;
     } else {  // FreeTriangle hit_info (generic.rs:78-92)
-        n = xyz(sc.ftri_n[idx]);
+        n = xyz(sc.ftri_n[idx - sc.pool_ftri]);
         pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
-        m = sc.ftri_mat + idx;
+        m = sc.ftri_mat + (idx - sc.pool_ftri);
     }
     const uint32_t divert = m->divert;
     bool seed_diff = false;
