@@ -125,8 +125,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if (info->width == 0 || info->height == 0) return set_err(c, RT_ERR_INVALID_ARG, "empty frame");
     if ((uint64_t)info->width * info->height >= (1ull << 31))
         return set_err(c, RT_ERR_INVALID_ARG, "frame too large");
-    if (info->dir_light_samp)
-        return set_err(c, RT_ERR_UNSUPPORTED, "dir_light_samp is not implemented on the device path");
 
     std::vector<Renderable> rs;
     int st = gather_renderables(scene, &rs);
@@ -165,6 +163,24 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
     std::vector<uint2> nodes(tree->n_nodes);
     for (uint32_t i = 0; i < tree->n_nodes; ++i) nodes[i] = make_uint2(tree->nodes[i].a, tree->nodes[i].b);
+
+    // Direct-light sampling (radiance.rs:89-120): every AABB'd renderable as a device ref in
+    // renderable order (the shadow ray's brute-force closest_ray_hit), and the emissive spheres
+    // with their position in that list.  Cube maps hit at +inf and can never be a shadow ray's
+    // first minimum ahead of a light, so they are left out.
+    std::vector<uint32_t> elem_refs;
+    std::vector<uint2> emit;
+    if (info->dir_light_samp) {
+        for (size_t ri = 0; ri < rs.size(); ++ri) {
+            if (!rs[ri].has_aabb) continue;
+            const uint32_t kind = rs[ri].kind == RT_KIND_SPHERE ? K_SPHERE : (rs[ri].kind == RT_KIND_FREE_TRI ? K_FREE_TRI : K_MESH_TRI);
+            const uint32_t base = kind == K_SPHERE ? 0u : (kind == K_FREE_TRI ? scene->n_spheres
+                                                                              : scene->n_spheres + scene->n_free_tris);
+            if (kind == K_SPHERE && scene->spheres[rs[ri].index].mat.has_emissive)
+                emit.push_back(make_uint2(rs[ri].index, (uint32_t)elem_refs.size()));
+            elem_refs.push_back((kind << REF_KIND_SHIFT) | (base + rs[ri].index));
+        }
+    }
 
     std::vector<float4> sph(scene->n_spheres);
     std::vector<DevMat> sph_mat(scene->n_spheres);
@@ -250,6 +266,11 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     HIPCHK(c, hipEventCreate(&c->ev0));
     HIPCHK(c, hipEventCreate(&c->ev1));
     if ((st = upload(c, nodes, &d.nodes))) return st;
+    if ((st = upload(c, elem_refs, &d.elem_refs))) return st;
+    if ((st = upload(c, emit, &d.emit))) return st;
+    d.n_elem_refs = (uint32_t)elem_refs.size();
+    d.n_emit = (uint32_t)emit.size();
+    d.dls = emit.empty() ? 0u : 1u;  // no emitter: the DLS term is exactly zero
     if ((st = upload(c, refs, &d.refs))) return st;
     if ((st = upload(c, sph, &d.sph))) return st;
     if ((st = upload(c, sph_mat, &d.sph_mat))) return st;
@@ -285,7 +306,8 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
     d.n_spheres = scene->n_spheres;
     // the sphere-only kernel reads every sphere from its LDS table (trace.hip fetch_sphere)
-    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty() && scene->n_spheres <= RT_LDS_SPHERES) ? 1u : 0u;
+    // (DLS runs in the general kernel)
+    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty() && scene->n_spheres <= RT_LDS_SPHERES && !d.dls) ? 1u : 0u;
     for (int i = 0; i < 6; ++i) d.bounds[i] = tree->bounds[i];
 
     // RayCompute::new (generate.rs:13-23)

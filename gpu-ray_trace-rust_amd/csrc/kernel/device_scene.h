@@ -74,6 +74,11 @@ struct DevScene {
     // A ref's index is its pool position; per-kind arrays below take index - pool_<kind>.
     const float4* prim4;
     uint32_t pool_ftri, pool_mesh;
+    // direct-light sampling (dir_light_samp): renderables in renderable order (device refs) and
+    // the emissive spheres {sphere index, position in elem_refs}
+    const uint32_t* elem_refs;
+    const uint2* emit;
+    uint32_t n_elem_refs, n_emit, dls;
     const float4* ftri_n;   // uniform normal
     const DevMat* ftri_mat;
     // mesh triangles (src/elements/mesh)

@@ -711,7 +711,50 @@ struct Path {
     V3 L, T;
     int depth;
     uint32_t rng;
+    // direct-light sampling (DLS kernels only): a DLS-eligible vertex waits for the next hit,
+    // the second index establish_dls_contrib omits (radiance.rs:48-52)
+    bool dls_on;
+    uint32_t dls_ref;
+    V3 dls_pos, dls_n, dls_T;
 };
+constexpr uint32_t REF_NONE = 0xfffffffeu;  // the continued ray hit nothing
+
+// establish_dls_contrib (radiance.rs:89-120) for the vertex held in p.dls_*: every emissive
+// sphere but the vertex's own element and `next` (the element the continued ray hit), seen
+// along d = normalize(c - pos) with d.n > 0, whose brute-force shadow ray over all renderables
+// returns that light as its first minimum, adds (d.n * emissive) * 1/(30 pi).  "First minimum
+// is the light" = the light has a valid hit l and no renderable before it (renderable order)
+// has a valid hit <= l, none after it one < l (closest_hit.rs:16-25; NaN never wins).
+__device__ V3 dls_contrib(const DevScene& sc, const Path& p, uint32_t next) {
+    const float NORMZE = 1.0f / (30.0f * PI);
+    V3 acc = mk(0.f, 0.f, 0.f);
+    for (uint32_t e = 0; e < sc.n_emit; ++e) {
+        const uint2 em = sc.emit[e];
+        const uint32_t eref = (K_SPHERE << REF_KIND_SHIFT) | em.x;
+        if (eref == p.dls_ref || eref == next) continue;
+        const float4 sp = sc.prim4[3 * (size_t)em.x];
+        const V3 d = normalize(xyz(sp) - p.dls_pos);
+        const float light_dot = dot(d, p.dls_n);
+        if (!(light_dot > 0.0f)) continue;
+        const Ray dr{d, p.dls_pos};
+        float li;
+        if (!sphere_hit(sp, dr, &li) || li < HIT_MIN) continue;
+        bool occluded = false;
+        for (uint32_t q = 0; q < sc.n_elem_refs && !occluded; ++q) {
+            if (q == em.y) continue;
+            const uint32_t ref = sc.elem_refs[q];
+            const float4* pd = sc.prim4 + 3 * (size_t)(ref & REF_INDEX_MASK);
+            float l = 0.f, bu, bv;
+            const bool h = (ref >> REF_KIND_SHIFT) == K_SPHERE ? sphere_hit(pd[0], dr, &l)
+                                                               : tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), dr, &l, &bu, &bv);
+            occluded = h && !(l < HIT_MIN) && (q < em.y ? l <= li : l < li);
+        }
+        if (occluded) continue;
+        const V3 emi = ld3(sc.sph_mat[em.x].em);
+        acc = acc + mk((light_dot * emi.x) * NORMZE, (light_dot * emi.y) * NORMZE, (light_dot * emi.z) * NORMZE);
+    }
+    return acc;
+}
 
 // tex_coord_from_bary (mesh/triangle.rs:228-237): sum from zero of coords[i_k] * b_k.
 __device__ __forceinline__ void tex_coord(const float2* uv, const DevMeshTri& t, float b1, float b2, float* u,
@@ -793,12 +836,17 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
 
 // Traces one segment of `p`.  Returns true when the path has ended (miss, cube map, Russian
 // roulette, debug_single_ray, bounce cap); p.L then holds the sample's radiance.
-template <bool COUNT, bool GEN>
+template <bool COUNT, bool GEN, bool DLS = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c) {
     if (COUNT) c.segments++;
     Hit h;
-    if (!closest<COUNT, GEN>(sc, k, p.ray, &h, st, c)) return true;  // miss: radiance 0
+    const bool hit = closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
+    if (DLS && p.dls_on) {  // the previous vertex's DLS term, now that its continued ray has hit
+        p.L = p.L + cmul(p.dls_T, dls_contrib(sc, p, hit ? h.ref : REF_NONE));
+        p.dls_on = false;
+    }
+    if (!hit) return true;  // miss: radiance 0
     if (COUNT) c.hits++;
     if (h.ref == REF_CUBE) {  // emissive only, no continue (distant_cube_map.rs:22,52-58)
         // (the reference still draws the RR uniform here; the stream ends with the path)
@@ -844,6 +892,14 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
     p.T = cmul(p.T, rgb);
     p.ray.d = nd;
     p.ray.o = pos;
+    // should_dls: diffuse spheres (Diff, or DiffSpec seeded diffuse); triangles never
+    if (DLS && kind == K_SPHERE && (divert == RT_DIVERT_DIFF || (divert == RT_DIVERT_DIFFSPEC && seed_diff))) {
+        p.dls_on = true;
+        p.dls_ref = h.ref;
+        p.dls_pos = pos;
+        p.dls_n = n;
+        p.dls_T = p.T;
+    }
     return ++p.depth >= MAX_BOUNCES;
 }
 
@@ -854,6 +910,7 @@ __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, i
     p.L = mk(0.f, 0.f, 0.f);
     p.T = mk(1.f, 1.f, 1.f);
     p.depth = 0;
+    p.dls_on = false;
 }
 
 // One lane = one pixel for the launch's whole sample range, with path regeneration: when a
@@ -863,7 +920,7 @@ __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, i
 // folded in sample order, exactly like draw_scene.rs:81-83.
 // GEN = false: the scene holds spheres only (and possibly a cube map); triangle and mesh code
 // is compiled out, which keeps the sphere kernel's register budget (walled.yml).
-template <bool COUNT, bool GEN>
+template <bool COUNT, bool GEN, bool DLS = false>
 #if RT_MIN_WAVES > 0
 __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a) {
 #else
@@ -909,7 +966,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     Path p;
     if (n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk);
     while (i < n_mine) {
-        if (segment<COUNT, GEN>(sc, k, p, st, c)) {
+        if (segment<COUNT, GEN, DLS>(sc, k, p, st, c)) {
             const uint32_t rel = kk + K * i;
             if (K == 1) {
                 const float n = (float)(a.sample_begin + rel);  // running mean, draw_scene.rs:81-83
@@ -975,7 +1032,7 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
     return g < 64u ? 64u : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
-template <bool GEN>
+template <bool GEN, bool DLS = false>
 #if RT_MIN_WAVES > 0
 __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
 #else
@@ -1041,7 +1098,7 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
             }
         }
         if (__ballot(have) == 0) break;
-        if (have && segment<false, GEN>(sc, k, p, st, c)) {
+        if (have && segment<false, GEN, DLS>(sc, k, p, st, c)) {
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;
             r[1] = p.L.y;
@@ -1084,21 +1141,27 @@ static size_t stack_lds_bytes(const LaunchArgs& a) {
 }
 
 hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
-    if (a.sc.spheres_only)
+    if (a.sc.dls)
+        hipLaunchKernelGGL((trace_kernel<false, true, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    else if (a.sc.spheres_only)
         hipLaunchKernelGGL((trace_kernel<false, false>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else
         hipLaunchKernelGGL((trace_kernel<false, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
-    if (a.sc.spheres_only)
+    if (a.sc.dls)
+        hipLaunchKernelGGL((queue_kernel<true, true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    else if (a.sc.spheres_only)
         hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else
         hipLaunchKernelGGL((queue_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s) {
-    if (a.sc.spheres_only)
+    if (a.sc.dls)
+        hipLaunchKernelGGL((trace_kernel<true, true, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+    else if (a.sc.spheres_only)
         hipLaunchKernelGGL((trace_kernel<true, false>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else
         hipLaunchKernelGGL((trace_kernel<true, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);

@@ -40,7 +40,7 @@ typedef enum rt_status {
     RT_ERR_INVALID_ARG = -1,   /* bad pointer / size / index (reference: assert!/expect panics) */
     RT_ERR_OOM = -2,           /* host or device allocation failed */
     RT_ERR_HIP = -3,           /* a HIP runtime call failed (message in rt_last_error) */
-    RT_ERR_UNSUPPORTED = -4,   /* feature not implemented on the device path (e.g. dir_light_samp) */
+    RT_ERR_UNSUPPORTED = -4,   /* beyond the device path (a KD tree deeper than its 64-entry stack) */
     RT_ERR_NO_DEVICE = -5,     /* no gfx950 device / bad device ordinal */
     RT_ERR_BATCH = -6          /* spp % batch != 0 (reference panic, src/renderer.rs:56-57) */
 } rt_status;
@@ -168,7 +168,7 @@ typedef struct rt_render_info {
     int32_t  assured_depth;    /* RussianRoullInfo::assured_depth */
     float    max_thres;        /* parsed but unused: radiance.rs:77 uses a static 0.4 */
     uint32_t debug_single_ray; /* RadianceInfo::debug_single_ray */
-    uint32_t dir_light_samp;   /* RadianceInfo::dir_light_samp (device path: RT_ERR_UNSUPPORTED) */
+    uint32_t dir_light_samp;   /* RadianceInfo::dir_light_samp (radiance.rs:46-56,89-120) */
     uint32_t _pad0;
     uint64_t seed;             /* rt_rng.h stream key */
 } rt_render_info;

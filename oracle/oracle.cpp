@@ -830,11 +830,23 @@ static RadOut radiance(const Ray& ray, const Scene& s, int depth, const RadInfo&
 }
 
 // The same estimator accumulated front to back (the device path's order).
+// Direct-light sampling (radiance.rs:46-56) needs the element the continued ray hits (the second
+// omitted index), so a vertex's DLS term is deferred: once the next segment's closest hit is
+// known, L += T_after_vertex (x) dls_contrib(vertex), before that segment's own emission.
 static V3 radiance_forward(Ray ray, const Scene& s, const RadInfo& ri) {
     V3 L = mk(0.f, 0.f, 0.f), T = mk(1.f, 1.f, 1.f);
+    bool pending = false;   // a DLS-eligible vertex waits for the next hit
+    HitInfo p_hi{};
+    Ray p_ray{};
+    uint32_t p_idx = 0;
+    V3 p_T = mk(0.f, 0.f, 0.f);
     for (int depth = 0;; ++depth) {
         COUNT(segments, 1);
         Closest c = s.kd.closest(ray);
+        if (pending) {
+            L = L + cmul(p_T, dls_contrib(s, p_idx, c.found ? (int)c.elem_idx : -1, p_hi, p_ray));
+            pending = false;
+        }
         if (!c.found) break;
         COUNT(hits, 1);
         const Element* elem = s.renderables[c.elem_idx];
@@ -850,6 +862,13 @@ static V3 radiance_forward(Ray ray, const Scene& s, const RadInfo& ri) {
         elem->continue_ray(ray, hi, &rgb, &nr);
         if (atten != 0.f) rgb = rgb / atten;
         T = cmul(T, rgb);
+        if (ri.dir_light_samp && hi.dls) {
+            pending = true;
+            p_hi = hi;
+            p_ray = ray;
+            p_idx = c.elem_idx;
+            p_T = T;
+        }
         ray = nr;
     }
     return L;
