@@ -1,0 +1,117 @@
+// rt_render — the reference's headless single-frame run (src/main.rs:14-43 with `no_ui`,
+// Renderer::consume_and_do renderer.rs:43-60, process_output_routine ui_util.rs:37-54) on the
+// MI355X device path, in C++ over the C ABI:
+//   scheme YAML -> rt_scheme_load -> rt_render_to_target (spp / gpu_render_batch launches)
+//   -> after every batch the RGBA8 target is flipped and saved as a PNG.
+// Usage: rt_render <scheme.yml|scheme.json> [no_ui] [--assets DIR] [--out FILE] [--device N]
+//                  [--seed S] [--width W] [--height H] [--spp N] [--batch B]
+// Assets are read from DIR/<dir>.npz (default: assets_pack next to the library's parent).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../../include/rt_abi.h"
+
+namespace {
+
+struct Out {
+    std::string path;
+    const uint8_t* target;
+    uint32_t w, h, spp;
+    int status = RT_OK;
+};
+
+void on_batch(void* user, uint32_t done) {
+    Out* o = static_cast<Out*>(user);
+    const int st = rt_write_png(o->path.c_str(), o->target, o->w, o->h, 1);
+    if (st != RT_OK) o->status = st;
+    std::fprintf(stderr, "\r[rt_render] %u / %u samples per pixel -> %s", done, o->spp, o->path.c_str());
+}
+
+int usage() {
+    std::fprintf(stderr,
+                 "usage: rt_render <scheme.yml|scheme.json> [no_ui] [--assets DIR] [--out FILE] [--device N]\n"
+                 "                 [--seed S] [--width W] [--height H] [--spp N] [--batch B]\n");
+    return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) return usage();
+    std::string scheme_path = argv[1], assets = "assets_pack", out = "render_out.png";
+    int device = 0;
+    unsigned long long seed = 0x5EED0001ull;
+    long width = -1, height = -1, spp = -1, batch = -1;
+    for (int i = 2; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto val = [&]() -> const char* {
+            if (i + 1 >= argc) {
+                std::fprintf(stderr, "%s needs a value\n", a.c_str());
+                std::exit(2);
+            }
+            return argv[++i];
+        };
+        if (a == "no_ui" || a == "ui") continue;  // main.rs:20-23: there is no UI here either way
+        else if (a == "--assets") assets = val();
+        else if (a == "--out") out = val();
+        else if (a == "--device") device = std::atoi(val());
+        else if (a == "--seed") seed = std::strtoull(val(), nullptr, 0);
+        else if (a == "--width") width = std::atol(val());
+        else if (a == "--height") height = std::atol(val());
+        else if (a == "--spp") spp = std::atol(val());
+        else if (a == "--batch") batch = std::atol(val());
+        else return usage();
+    }
+    std::ifstream f(scheme_path);
+    if (!f) {
+        std::fprintf(stderr, "Couldn't open file %s\n", scheme_path.c_str());
+        return 1;
+    }
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string text = ss.str();
+    const bool json = scheme_path.size() > 5 && scheme_path.compare(scheme_path.size() - 5, 5, ".json") == 0;
+    rt_scheme* sch = nullptr;
+    int st = rt_scheme_load(text.data(), text.size(), json ? RT_SCHEME_JSON : RT_SCHEME_YAML, assets.c_str(), seed, &sch);
+    if (st != RT_OK) {
+        std::fprintf(stderr, "rt_render: %s: %s\n", rt_status_string(st), rt_scheme_last_error());
+        return 1;
+    }
+    rt_scheme_view v{};
+    rt_scheme_view_get(sch, &v);
+    if (v.animation) {
+        std::fprintf(stderr, "rt_render: animation schemes are not supported (renderer.rs:65-207)\n");
+        rt_scheme_free(sch);
+        return 1;
+    }
+    if (!v.use_gpu)
+        std::fprintf(stderr, "rt_render: use_gpu is false in the scheme; rendering on the device path anyway\n");
+    if (width > 0) v.info->width = (uint32_t)width;
+    if (height > 0) v.info->height = (uint32_t)height;
+    const uint32_t n_spp = spp > 0 ? (uint32_t)spp : v.samps_per_pix;
+    const uint32_t n_batch = batch > 0 ? (uint32_t)batch : v.gpu_render_batch;
+    if (!n_batch) {
+        std::fprintf(stderr, "rt_render: gpu_render_batch needs to be set for GPU mode!\n");  // renderer.rs:55
+        rt_scheme_free(sch);
+        return 1;
+    }
+    std::vector<uint8_t> target((size_t)v.info->width * v.info->height * 4, 0);
+    Out o{out, target.data(), v.info->width, v.info->height, n_spp};
+    st = rt_render_to_target(v.scene, v.cam, v.info, n_spp, n_batch, device, target.data(), on_batch, &o);
+    std::fprintf(stderr, "\n");
+    rt_scheme_free(sch);
+    if (st != RT_OK) {
+        std::fprintf(stderr, "rt_render: %s\n", rt_status_string(st));
+        return 1;
+    }
+    if (o.status != RT_OK) {
+        std::fprintf(stderr, "rt_render: cannot save %s\n", out.c_str());
+        return 1;
+    }
+    return 0;
+}

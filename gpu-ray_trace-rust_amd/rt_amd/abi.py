@@ -116,6 +116,15 @@ class rt_work_counts(C.Structure):
                                            "tri_tests", "hits", "mesh_hits")]
 
 
+RT_SCHEME_YAML, RT_SCHEME_JSON = 0, 1
+
+
+class rt_scheme_view(C.Structure):
+    _fields_ = [("scene", C.POINTER(rt_scene_desc)), ("cam", C.POINTER(rt_camera)),
+                ("info", C.POINTER(rt_render_info)), ("samps_per_pix", C.c_uint32),
+                ("gpu_render_batch", C.c_uint32), ("use_gpu", C.c_uint32), ("animation", C.c_uint32)]
+
+
 # Every symbol the header declares (tests/test_abi.py checks the library exports them all).
 EXPORTS = {
     "rt_abi_version": (C.c_int, []),
@@ -142,6 +151,12 @@ EXPORTS = {
     "rt_render_to_target": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(rt_camera),
                                       C.POINTER(rt_render_info), C.c_uint32, C.c_uint32, C.c_int,
                                       C.POINTER(C.c_uint8), C.c_void_p, C.c_void_p]),
+    "rt_scheme_load": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint32, C.c_char_p, C.c_uint64,
+                                 C.POINTER(C.c_void_p)]),
+    "rt_scheme_view_get": (C.c_int, [C.c_void_p, C.POINTER(rt_scheme_view)]),
+    "rt_scheme_last_error": (C.c_char_p, []),
+    "rt_scheme_free": (C.c_int, [C.c_void_p]),
+    "rt_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32, C.c_uint32]),
 }
 
 _LIB = None

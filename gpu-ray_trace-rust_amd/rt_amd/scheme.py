@@ -279,3 +279,43 @@ def load(scheme: dict, assets_root: str | None = None, seed: int = DEFAULT_SEED,
     return LoadedScheme(scheme=scheme, scene=sc, desc=desc, cam=camera(scheme["cam"], lib),
                         info=render_info(ri, seed, width, height), spp=int(ri["samps_per_pix"]),
                         batch=ri.get("gpu_render_batch"))
+
+
+class NativeScheme:
+    """A scheme loaded by the C++ host (rt_scheme_load): the same LoadedScheme fields, with the
+    description owned by the library.  `text` is YAML or this repo's JSON form."""
+
+    def __init__(self, text: str, assets_root: str | None, fmt: int | None = None, seed: int = DEFAULT_SEED,
+                 width: int | None = None, height: int | None = None, lib=None):
+        self.lib = lib or abi.load_library()
+        if fmt is None:
+            fmt = abi.RT_SCHEME_JSON if text.lstrip().startswith("{") else abi.RT_SCHEME_YAML
+        raw = text.encode()
+        self.ptr = C.c_void_p()
+        st = self.lib.rt_scheme_load(raw, len(raw), fmt, assets_root.encode() if assets_root else None, int(seed),
+                                     C.byref(self.ptr))
+        if st != abi.RT_OK:
+            raise abi.RtError(st, (self.lib.rt_scheme_last_error() or b"").decode())
+        v = abi.rt_scheme_view()
+        abi.check(self.lib, self.lib.rt_scheme_view_get(self.ptr, C.byref(v)))
+        self.view = v
+        self.desc = v.scene.contents
+        self.cam = v.cam.contents
+        self.info = v.info.contents
+        if width is not None:
+            self.info.width = int(width)
+        if height is not None:
+            self.info.height = int(height)
+        self.spp = int(v.samps_per_pix)
+        self.batch = int(v.gpu_render_batch) or None
+
+    def close(self):
+        if self.ptr:
+            self.lib.rt_scheme_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -284,6 +284,36 @@ int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* cam,
                         const rt_render_info* info, uint32_t spp, uint32_t batch,
                         int device, uint8_t* target, rt_update_hook hook, void* user);
 
+/* ------------------------------------------------------------ host: the boundary's caller */
+/* Scheme loading in C++ (what the reference's builder does before the `use_gpu` switch):
+ * Scheme::from_yml + apply_corrections (builder/mod.rs:63-72), member conversion in renderable
+ * order (builder/inner.rs:21-64), glTF models (builder/pr/model.rs:19-207) and cube-map images
+ * (builder/pr/distant_cube_map.rs:19-23), reading assets from `assets_root`/<dir>.npz (the
+ * repo's asset packs).  `text` is the scheme YAML (RT_SCHEME_YAML) or its JSON form
+ * (RT_SCHEME_JSON: tags as {"!Tag": value}).  The scheme owns every array its view points
+ * into; the view's info / cam may be edited before rt_create (e.g. width / height overrides). */
+typedef struct rt_scheme rt_scheme;
+enum { RT_SCHEME_YAML = 0, RT_SCHEME_JSON = 1 };
+typedef struct rt_scheme_view {
+    const rt_scene_desc* scene;
+    rt_camera*           cam;
+    rt_render_info*      info;
+    uint32_t             samps_per_pix;
+    uint32_t             gpu_render_batch;   /* 0 when absent (Option<u32>) */
+    uint32_t             use_gpu;            /* RenderInfo::use_gpu.unwrap_or(false) */
+    uint32_t             animation;          /* RenderInfo::animation.unwrap_or(false) */
+} rt_scheme_view;
+int         rt_scheme_load(const char* text, uint64_t len, uint32_t format, const char* assets_root,
+                           uint64_t seed, rt_scheme** out);
+int         rt_scheme_view_get(rt_scheme* scheme, rt_scheme_view* out);
+const char* rt_scheme_last_error(void);   /* this thread's last rt_scheme_load failure */
+int         rt_scheme_free(rt_scheme* scheme);
+
+/* process_output_routine (ui_util.rs:37-54): an RGBA8 buffer (width*height*4, row y = pixel
+ * row y of the target) saved as an 8-bit RGBA PNG, flipped vertically when flip_vertical. */
+int rt_write_png(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height,
+                 uint32_t flip_vertical);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,7 +5,7 @@
 set -e
 PKG=$(dirname "$0")/../gpu-ray_trace-rust_amd
 cd "$PKG"
-make -s build/kd_build.o build/mesh_flatten.o
+make -s build/kd_build.o build/mesh_flatten.o build/doc.o build/pack.o build/scheme_host.o
 mkdir -p lib/variants build/variants
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-rdc -munsafe-fp-atomics"
 for spec in "$@"; do
@@ -13,6 +13,6 @@ for spec in "$@"; do
   hipcc $FLAGS $defs -c -o build/variants/trace_$name.o csrc/kernel/trace.hip &
   hipcc $FLAGS $defs -c -o build/variants/runtime_$name.o csrc/host/runtime.hip &
   wait
-  hipcc --offload-arch=gfx950 -shared -o lib/variants/librt_$name.so build/kd_build.o build/mesh_flatten.o build/variants/runtime_$name.o build/variants/trace_$name.o
+  hipcc --offload-arch=gfx950 -shared -o lib/variants/librt_$name.so build/kd_build.o build/mesh_flatten.o build/doc.o build/pack.o build/scheme_host.o build/variants/runtime_$name.o build/variants/trace_$name.o -lz
   echo "built $name: $defs"
 done

@@ -2,9 +2,8 @@
 
 The GPU box receives only this repository.  Each pack holds, for one directory of the
 reference's assets/: every glTF document's JSON ("gltf:<name>") and binary buffers
-("buf:<name>:<i>"), every PNG decoded to 8-bit channels ("img:<relpath>", by
-rt_amd.assets.decode_image — the decode the file store uses) and every JPEG as its encoded
-bytes ("jpg:<relpath>", decoded at load by the same function).  Run in this container:
+("buf:<name>:<i>"), every PNG and JPEG decoded to 8-bit channels ("img:<relpath>", by
+rt_amd.assets.decode_image — the decode the file store uses).  Run in this container:
     python tools/make_asset_packs.py [dirs...]
 """
 import json
@@ -36,10 +35,9 @@ def pack(d):
                     bp = os.path.join(os.path.dirname(full), b["uri"])
                     if os.path.exists(bp):
                         out[f"buf:{rel}:{i}"] = np.frombuffer(open(bp, "rb").read(), dtype=np.uint8)
-            elif f.lower().endswith((".jpg", ".jpeg")):
-                # JPEGs stay encoded (decoded at load by the same PIL decoder as the file store)
-                out["jpg:" + rel] = np.frombuffer(open(full, "rb").read(), dtype=np.uint8)
             elif f.lower().endswith(IMG_EXT):
+                # PNG and JPEG alike are stored decoded (one decoder, PIL, for both hosts: the
+                # C++ host has no JPEG decoder)
                 out["img:" + rel] = decode_image(open(full, "rb").read())
     os.makedirs(os.path.join(ROOT, "assets_pack"), exist_ok=True)
     dst = os.path.join(ROOT, "assets_pack", d + ".npz")
