@@ -26,23 +26,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-STRIPE = 4  # rows; fine interleave balances sky-vs-geometry cost across ranks
 # Canonical per-event byte sizes of the roofline
 BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits": 32, "mesh_hits": 132}
 
 
-def rank_tiles(width, height, rank, world):
-    """STRIPE-row stripes dealt round-robin; consecutive stripes of one rank merge."""
-    tiles = []
-    for i, y0 in enumerate(range(0, height, STRIPE)):
-        if i % world == rank:
-            hh = min(STRIPE, height - y0)
-            if tiles and tiles[-1][1] + tiles[-1][3] == y0:
-                x, yy, ww, h0 = tiles[-1]
-                tiles[-1] = (x, yy, ww, h0 + hh)
-            else:
-                tiles.append((0, y0, width, hh))
-    return tiles
+from rt_amd.shard import STRIPE, max_rank_pixels, rank_tiles  # noqa: E402
 
 
 def roofline_bytes_per_sample(ctx, width, height, spp=16, device=False):
@@ -146,8 +134,7 @@ def main():
         shard_rank, shard_world = (int(v) for v in args.as_rank.split("/"))
     tiles = rank_tiles(w, h, shard_rank, shard_world)
     npix = sum(t[2] * t[3] for t in tiles)
-    max_npix = max(sum(t[2] * t[3] for t in rank_tiles(w, h, r, world)) for r in range(world))
-    max_npix = max(max_npix, npix)
+    max_npix = max(max_rank_pixels(w, h, world), npix)
 
     ctx = render.Context(loaded, device=local)
     out = torch.zeros((max_npix, 4), dtype=torch.float32, device=f"cuda:{local}")
@@ -186,6 +173,14 @@ def main():
         t = torch.tensor([elapsed], device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # after the timed region: rank 0 reassembles the last gathered frame (rt_amd/shard.py) and
+    # checks that every pixel was rendered by some rank (alpha is 1 exactly where written)
+    frame_complete = None
+    if not args.as_rank and rank == 0:
+        from rt_amd import shard
+
+        frame = shard.assemble(gather if dist else [out], w, h, world)
+        frame_complete = bool((frame[..., 3] == 1.0).all().item())
 
     total_samples = (npix if args.as_rank else w * h) * spp_rank * args.steps
     value = total_samples / elapsed / 1e6
@@ -198,6 +193,7 @@ def main():
                                   f"kd_tree_depth {int(loaded.info.kd_tree_depth)}",
                       "spp_per_step": spp, "pixels": w * h, "stripes": f"{STRIPE}-row round-robin",
                       "parallelism": f"tiles{world}"}}
+    res["frame_complete"] = frame_complete
     res["launch"] = {"trace_launches_per_step": n_launch / args.steps,
                      "samples_per_launch": round(npix * spp_rank * args.steps / max(n_launch, 1))}
     if args.as_rank:
