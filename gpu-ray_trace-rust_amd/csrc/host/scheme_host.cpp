@@ -12,6 +12,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <functional>
@@ -182,6 +183,17 @@ struct rt_scheme {
     rt_camera cam{};
     rt_render_info info{};
     uint32_t spp = 0, batch = 0, use_gpu = 0, animation = 0;
+    // kept to build animation frames (rt_scheme_frame)
+    NodeP root;
+    std::string assets_root;
+    bool has_assets = false;
+    uint64_t seed = 0;
+};
+
+// Per-member replacement values of one animation frame (extract_anim, inner.rs:113-210).
+struct MemberOverride {
+    bool c = false, trans = false, euler = false;
+    float cv[3], tv[3], ev[3];
 };
 
 namespace {
@@ -250,7 +262,7 @@ uint32_t comp_u32(const Accessor& a, uint32_t i) {
     throw std::runtime_error("glTF: index component type");
 }
 
-void load_model(rt_scheme* s, const Node* model, rth::PackStore& store) {  // Model::to_meshes
+void load_model(rt_scheme* s, const Node* model, rth::PackStore& store, const MemberOverride* o) {  // Model::to_meshes
     std::string dir, rel;
     rth::PackStore::split(need(model, "path")->str(), &dir, &rel);
     const rth::NpzFile* pk = store.pack(dir);
@@ -281,6 +293,8 @@ void load_model(rt_scheme* s, const Node* model, rth::PackStore& store) {  // Mo
     float t[3], e[3];
     v3(need(model, "translation"), t);
     v3(need(model, "euler_angles"), e);
+    if (o && o->trans) std::memcpy(t, o->tv, sizeof(t));
+    if (o && o->euler) std::memcpy(e, o->ev, sizeof(e));
     const float sc = f32(need(model, "uniform_scale"));
     M4 T = eye4(), S = eye4();
     T.m[0][3] = t[0];
@@ -376,7 +390,8 @@ void load_model(rt_scheme* s, const Node* model, rth::PackStore& store) {  // Mo
                 for (const NodeP& n : nodes->seq) explore((size_t)n->num(), transform);
 }
 
-void build(rt_scheme* s, const Node* root, const char* assets_root, uint64_t seed) {
+void build(rt_scheme* s, const Node* root, const char* assets_root, uint64_t seed,
+           const std::vector<MemberOverride>* ov = nullptr) {
     const Node* ri = need(root, "render_info");
     s->info.width = (uint32_t)need(ri, "width")->num();
     s->info.height = (uint32_t)need(ri, "height")->num();
@@ -408,12 +423,15 @@ void build(rt_scheme* s, const Node* root, const char* assets_root, uint64_t see
 
     rth::PackStore store(assets_root ? assets_root : "");
     std::map<std::string, int> tex_cache;
-    for (const NodeP& m : need(root, "scene_members")->seq) {  // inner.rs:21-64, member order
+    const Node* members = need(root, "scene_members");
+    for (size_t mi = 0; mi < members->seq.size(); ++mi) {  // inner.rs:21-64, member order
         const Node* v = nullptr;
-        const std::string kind = tag_of(m.get(), &v);
+        const std::string kind = tag_of(members->seq[mi].get(), &v);
+        const MemberOverride* o = ov && mi < ov->size() ? &(*ov)[mi] : nullptr;
         if (kind == "Sphere") {
             rt_sphere sp{};
             v3(need(v, "c"), sp.c);
+            if (o && o->c) std::memcpy(sp.c, o->cv, sizeof(sp.c));
             sp.r = f32(need(v, "r"));
             const Node* cv = nullptr;
             if (tag_of(need(v, "coloring"), &cv) != "Solid") throw std::runtime_error("unknown coloring");
@@ -453,7 +471,7 @@ void build(rt_scheme* s, const Node* root, const char* assets_root, uint64_t see
             s->cube_maps.push_back(cm);
         } else if (kind == "Model") {
             if (!assets_root) throw std::runtime_error("Model needs an assets root");
-            load_model(s, v, store);
+            load_model(s, v, store, o);
         } else {
             throw std::runtime_error("unknown scene member " + kind);
         }
@@ -508,7 +526,220 @@ extern "C" int rt_scheme_load(const char* text, uint64_t len, uint32_t format, c
         const NodeP root = format == RT_SCHEME_YAML ? rth::parse_yaml(src) : rth::parse_json(src);
         std::unique_ptr<rt_scheme> s(new rt_scheme());
         build(s.get(), root.get(), assets_root, seed);
+        s->root = root;
+        s->has_assets = assets_root != nullptr;
+        s->assets_root = assets_root ? assets_root : "";
+        s->seed = seed;
         *out = s.release();
+        return RT_OK;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return RT_ERR_OOM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return RT_ERR_INVALID_ARG;
+    }
+}
+
+// ------------------------------------------------------------------------------ animation
+// extract_anim (builder/inner.rs:113-210) over keyframe 1.1.1's AnimationSequence.  The crate
+// is not vendored: its sequence and easing arithmetic are restated from its published behaviour
+// (parity unpinned): keyframes sorted by time; the value at time t tweens from the last
+// keyframe at or before t to the next one with the *earlier* keyframe's easing function of the
+// clamped progress (t - t0) / (t1 - t0); the tween is per component in f64, from + (to - from) y,
+// rounded to f32; at or past the last keyframe its value holds.  advance_by adds the frame
+// period to an f64 clock clamped to [0, last keyframe time].
+namespace {
+
+double ease_y(const std::string& f, double x) {
+    auto bezier = [](double x1, double y1, double x2, double y2, double x) {  // CSS cubic-bezier
+        auto bx = [&](double t) { return 3 * (1 - t) * (1 - t) * t * x1 + 3 * (1 - t) * t * t * x2 + t * t * t; };
+        auto by = [&](double t) { return 3 * (1 - t) * (1 - t) * t * y1 + 3 * (1 - t) * t * t * y2 + t * t * t; };
+        double lo = 0.0, hi = 1.0, t = x;
+        for (int i = 0; i < 64; ++i) {  // bisection to full double precision
+            t = 0.5 * (lo + hi);
+            if (bx(t) < x) lo = t;
+            else hi = t;
+        }
+        return by(t);
+    };
+    if (f == "Linear") return x;
+    if (f == "Step") return x < 0.5 ? 0.0 : 1.0;
+    if (f == "Hold") return x < 1.0 ? 0.0 : 1.0;
+    if (f == "EaseIn") return bezier(0.42, 0.0, 1.0, 1.0, x);
+    if (f == "EaseOut") return bezier(0.0, 0.0, 0.58, 1.0, x);
+    if (f == "EaseInOut") return bezier(0.42, 0.0, 0.58, 1.0, x);
+    if (f == "EaseInQuad") return x * x;
+    if (f == "EaseOutQuad") return -x * (x - 2.0);
+    if (f == "EaseInOutQuad") return x < 0.5 ? 2.0 * x * x : -2.0 * x * x + 4.0 * x - 1.0;
+    if (f == "EaseInCubic") return x * x * x;
+    if (f == "EaseOutCubic") { const double y = x - 1.0; return y * y * y + 1.0; }
+    if (f == "EaseInOutCubic") {
+        if (x < 0.5) return 4.0 * x * x * x;
+        const double y = 2.0 * x - 2.0;
+        return 0.5 * y * y * y + 1.0;
+    }
+    if (f == "EaseInQuart") return x * x * x * x;
+    if (f == "EaseOutQuart") { const double y = x - 1.0; return -(y * y * y * y - 1.0); }
+    if (f == "EaseInOutQuart") {
+        if (x < 0.5) return 8.0 * x * x * x * x;
+        const double y = x - 1.0;
+        return -8.0 * y * y * y * y + 1.0;
+    }
+    if (f == "EaseInQuint") return x * x * x * x * x;
+    if (f == "EaseOutQuint") { const double y = x - 1.0; return y * y * y * y * y + 1.0; }
+    if (f == "EaseInOutQuint") {
+        if (x < 0.5) return 16.0 * x * x * x * x * x;
+        const double y = x - 1.0;
+        return 16.0 * y * y * y * y * y + 1.0;
+    }
+    throw std::runtime_error("Unsupported easing function: " + f);  // builder/mod.rs:58
+}
+
+struct Key {
+    double time;
+    float v[6];       // translation, euler angles
+    std::string ease; // Keyframe::get_ease_type, default EaseInOut (builder/mod.rs:38)
+};
+
+struct Sequence {
+    std::vector<Key> keys;
+    double clock = 0.0;
+    double duration() const { return keys.empty() ? 0.0 : keys.back().time; }
+    void advance_by(double dt) {
+        double t = clock + dt;
+        clock = t < 0.0 ? 0.0 : (t > duration() ? duration() : t);
+    }
+    void now(int n, float* out) const {
+        size_t k = 0;
+        bool found = false;
+        for (size_t i = 0; i < keys.size(); ++i)
+            if (keys[i].time <= clock) {
+                k = i;
+                found = true;
+            }
+        if (!found) {
+            for (int c = 0; c < n; ++c) out[c] = keys.front().v[c];
+            return;
+        }
+        if (k + 1 >= keys.size()) {
+            for (int c = 0; c < n; ++c) out[c] = keys[k].v[c];
+            return;
+        }
+        const Key &a = keys[k], &b = keys[k + 1];
+        double x = (clock - a.time) / (b.time - a.time);
+        x = x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
+        const double y = ease_y(a.ease, x);
+        for (int c = 0; c < n; ++c) out[c] = (float)((double)a.v[c] + ((double)b.v[c] - (double)a.v[c]) * y);
+    }
+};
+
+// the member's keyframe sequence, or false when it has no animation
+bool member_sequence(const Node* v, bool model, Sequence* seq) {
+    const Node* anim = v->get("animation");
+    if (!anim || anim->kind == Node::Null) return false;
+    for (const NodeP& kf : need(anim, "keyframes")->seq) {
+        Key k{};
+        k.time = (double)f32(need(kf.get(), "time"));
+        v3(need(kf.get(), "translation"), k.v);
+        if (model) {
+            const Node* e = kf->get("euler_angles");
+            if (!e || e->kind == Node::Null) throw std::runtime_error("model keyframe without euler_angles");
+            v3(e, k.v + 3);
+        }
+        const Node* et = kf->get("ease_type");
+        k.ease = et && et->kind != Node::Null ? et->str() : "EaseInOut";
+        (void)ease_y(k.ease, 0.0);  // unknown names fail at load, as get_ease_type panics
+        for (const Key& o : seq->keys)
+            if (o.time == k.time) throw std::runtime_error("two keyframes at the same time");
+        seq->keys.push_back(k);
+    }
+    std::stable_sort(seq->keys.begin(), seq->keys.end(), [](const Key& a, const Key& b) { return a.time < b.time; });
+    return true;
+}
+
+// number_of_frames and the per-member sequences (extract_anim, inner.rs:113-124)
+uint32_t frame_plan(const rt_scheme* s, std::vector<std::pair<int, Sequence>>* seqs, double* tpf) {
+    const Node* root = s->root.get();
+    const Node* ri = need(root, "render_info");
+    const Node* members = need(root, "scene_members");
+    float last = 0.0f;
+    bool any = false;
+    for (size_t mi = 0; mi < members->seq.size(); ++mi) {
+        const Node* v = nullptr;
+        const std::string kind = tag_of(members->seq[mi].get(), &v);
+        if (kind != "Sphere" && kind != "Model") continue;
+        Sequence q;
+        if (!member_sequence(v, kind == "Model", &q)) {
+            any = true;
+            continue;
+        }
+        // get_last_timestamp: the member's last keyframe in file order, reduced with f32::max
+        const Node* kfs = need(v->get("animation"), "keyframes");
+        const float t = f32(need(kfs->seq.back().get(), "time"));
+        last = any ? std::fmax(last, t) : t;
+        any = true;
+        seqs->emplace_back((int)mi, std::move(q));
+    }
+    const Node* fr = ri->get("framerate");
+    if (!fr || fr->kind == Node::Null) throw std::runtime_error("Ensure the framerate is added for use_gpu!");
+    *tpf = 1.0 / (double)f32(fr);
+    return (uint32_t)((double)last / *tpf);
+}
+
+}  // namespace
+
+extern "C" int rt_scheme_frames(rt_scheme* s, uint32_t* n_frames) {
+    if (!s || !n_frames) return RT_ERR_INVALID_ARG;
+    *n_frames = 0;
+    if (!s->animation) return RT_OK;
+    try {
+        std::vector<std::pair<int, Sequence>> seqs;
+        double tpf;
+        *n_frames = frame_plan(s, &seqs, &tpf);
+        return RT_OK;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return RT_ERR_INVALID_ARG;
+    }
+}
+
+extern "C" int rt_scheme_frame(rt_scheme* s, uint32_t frame, rt_scheme** out) {
+    if (!s || !out || !s->animation) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    try {
+        std::vector<std::pair<int, Sequence>> seqs;
+        double tpf;
+        const uint32_t n = frame_plan(s, &seqs, &tpf);
+        if (frame >= n) return RT_ERR_INVALID_ARG;
+        const Node* members = need(s->root.get(), "scene_members");
+        std::vector<MemberOverride> ov(members->seq.size());
+        for (auto& ms : seqs) {
+            Sequence& q = ms.second;
+            for (uint32_t i = 0; i < frame; ++i) q.advance_by(tpf);  // one advance per frame
+            const Node* v = nullptr;
+            const bool model = tag_of(members->seq[(size_t)ms.first].get(), &v) == "Model";
+            float val[6];
+            q.now(model ? 6 : 3, val);
+            MemberOverride& o = ov[(size_t)ms.first];
+            if (model) {
+                o.trans = o.euler = true;
+                std::memcpy(o.tv, val, sizeof(o.tv));
+                std::memcpy(o.ev, val + 3, sizeof(o.ev));
+            } else {
+                o.c = true;
+                std::memcpy(o.cv, val, sizeof(o.cv));
+            }
+        }
+        std::unique_ptr<rt_scheme> f(new rt_scheme());
+        build(f.get(), s->root.get(), s->has_assets ? s->assets_root.c_str() : nullptr, s->seed, &ov);
+        f->info = s->info;  // the caller's overrides (size, flags) carry over
+        f->root = s->root;
+        f->has_assets = s->has_assets;
+        f->assets_root = s->assets_root;
+        f->seed = s->seed;
+        f->animation = 0;   // a frame is a still scene
+        *out = f.release();
         return RT_OK;
     } catch (const std::bad_alloc&) {
         g_err = "out of host memory";

@@ -3,13 +3,19 @@
 // MI355X device path, in C++ over the C ABI:
 //   scheme YAML -> rt_scheme_load -> rt_render_to_target (spp / gpu_render_batch launches)
 //   -> after every batch the RGBA8 target is flipped and saved as a PNG.
+// Animated schemes (render_info.animation, renderer.rs:65-207) render every frame to
+// <frames-dir>/<n>.png, n from 1 as in the GPU branch; --frames r/N renders frames i with
+// i % N == r (frames are independent: N processes on N GPUs need no collective).  The mp4
+// muxing of main.rs:54-97 (openh264) is not reproduced.
 // Usage: rt_render <scheme.yml|scheme.json> [no_ui] [--assets DIR] [--out FILE] [--device N]
 //                  [--seed S] [--width W] [--height H] [--spp N] [--batch B]
+//                  [--frames-dir DIR] [--frames r/N] [--max-frames K]
 // Assets are read from DIR/<dir>.npz (default: assets_pack next to the library's parent).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <sys/stat.h>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -35,7 +41,8 @@ void on_batch(void* user, uint32_t done) {
 int usage() {
     std::fprintf(stderr,
                  "usage: rt_render <scheme.yml|scheme.json> [no_ui] [--assets DIR] [--out FILE] [--device N]\n"
-                 "                 [--seed S] [--width W] [--height H] [--spp N] [--batch B]\n");
+                 "                 [--seed S] [--width W] [--height H] [--spp N] [--batch B]\n"
+                 "                 [--frames-dir DIR] [--frames r/N] [--max-frames K]\n");
     return 2;
 }
 
@@ -46,7 +53,9 @@ int main(int argc, char** argv) {
     std::string scheme_path = argv[1], assets = "assets_pack", out = "render_out.png";
     int device = 0;
     unsigned long long seed = 0x5EED0001ull;
-    long width = -1, height = -1, spp = -1, batch = -1;
+    long width = -1, height = -1, spp = -1, batch = -1, max_frames = -1;
+    std::string frames_dir = "anim_frames";
+    unsigned frank = 0, fworld = 1;
     for (int i = 2; i < argc; ++i) {
         const std::string a = argv[i];
         auto val = [&]() -> const char* {
@@ -65,6 +74,11 @@ int main(int argc, char** argv) {
         else if (a == "--height") height = std::atol(val());
         else if (a == "--spp") spp = std::atol(val());
         else if (a == "--batch") batch = std::atol(val());
+        else if (a == "--frames-dir") frames_dir = val();
+        else if (a == "--max-frames") max_frames = std::atol(val());
+        else if (a == "--frames") {
+            if (std::sscanf(val(), "%u/%u", &frank, &fworld) != 2 || fworld == 0 || frank >= fworld) return usage();
+        }
         else return usage();
     }
     std::ifstream f(scheme_path);
@@ -84,11 +98,6 @@ int main(int argc, char** argv) {
     }
     rt_scheme_view v{};
     rt_scheme_view_get(sch, &v);
-    if (v.animation) {
-        std::fprintf(stderr, "rt_render: animation schemes are not supported (renderer.rs:65-207)\n");
-        rt_scheme_free(sch);
-        return 1;
-    }
     if (!v.use_gpu)
         std::fprintf(stderr, "rt_render: use_gpu is false in the scheme; rendering on the device path anyway\n");
     if (width > 0) v.info->width = (uint32_t)width;
@@ -99,6 +108,39 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "rt_render: gpu_render_batch needs to be set for GPU mode!\n");  // renderer.rs:55
         rt_scheme_free(sch);
         return 1;
+    }
+    if (v.animation) {  // consume_and_do_anim (renderer.rs:65-207)
+        uint32_t n = 0;
+        if ((st = rt_scheme_frames(sch, &n)) != RT_OK) {
+            std::fprintf(stderr, "rt_render: %s\n", rt_scheme_last_error());
+            rt_scheme_free(sch);
+            return 1;
+        }
+        if (max_frames >= 0 && (uint32_t)max_frames < n) n = (uint32_t)max_frames;
+        ::mkdir(frames_dir.c_str(), 0755);
+        std::fprintf(stderr, "rt_render: %u frames, rank %u of %u\n", n, frank, fworld);
+        for (uint32_t i = frank; i < n; i += fworld) {
+            rt_scheme* fr = nullptr;
+            if ((st = rt_scheme_frame(sch, i, &fr)) != RT_OK) {
+                std::fprintf(stderr, "rt_render: frame %u: %s\n", i, rt_scheme_last_error());
+                rt_scheme_free(sch);
+                return 1;
+            }
+            rt_scheme_view fv{};
+            rt_scheme_view_get(fr, &fv);
+            std::vector<uint8_t> target((size_t)fv.info->width * fv.info->height * 4, 0);
+            Out o{frames_dir + "/" + std::to_string(i + 1) + ".png", target.data(), fv.info->width, fv.info->height, n_spp};
+            st = rt_render_to_target(fv.scene, fv.cam, fv.info, n_spp, n_batch, device, target.data(), on_batch, &o);
+            rt_scheme_free(fr);
+            std::fprintf(stderr, "\n");
+            if (st != RT_OK || o.status != RT_OK) {
+                std::fprintf(stderr, "rt_render: frame %u: %s\n", i, rt_status_string(st != RT_OK ? st : o.status));
+                rt_scheme_free(sch);
+                return 1;
+            }
+        }
+        rt_scheme_free(sch);
+        return 0;
     }
     std::vector<uint8_t> target((size_t)v.info->width * v.info->height * 4, 0);
     Out o{out, target.data(), v.info->width, v.info->height, n_spp};

@@ -156,6 +156,8 @@ EXPORTS = {
     "rt_scheme_view_get": (C.c_int, [C.c_void_p, C.POINTER(rt_scheme_view)]),
     "rt_scheme_last_error": (C.c_char_p, []),
     "rt_scheme_free": (C.c_int, [C.c_void_p]),
+    "rt_scheme_frames": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "rt_scheme_frame": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rt_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32, C.c_uint32]),
 }
 

@@ -309,6 +309,32 @@ class NativeScheme:
         self.spp = int(v.samps_per_pix)
         self.batch = int(v.gpu_render_batch) or None
 
+    @classmethod
+    def _wrap(cls, lib, ptr):
+        self = cls.__new__(cls)
+        self.lib, self.ptr = lib, ptr
+        v = abi.rt_scheme_view()
+        abi.check(lib, lib.rt_scheme_view_get(ptr, C.byref(v)))
+        self.view, self.desc, self.cam, self.info = v, v.scene.contents, v.cam.contents, v.info.contents
+        self.spp, self.batch = int(v.samps_per_pix), int(v.gpu_render_batch) or None
+        return self
+
+    def n_frames(self) -> int:
+        """rt_scheme_frames: frames of an animated scheme (0 otherwise)."""
+        n = C.c_uint32()
+        st = self.lib.rt_scheme_frames(self.ptr, C.byref(n))
+        if st != abi.RT_OK:
+            raise abi.RtError(st, (self.lib.rt_scheme_last_error() or b"").decode())
+        return int(n.value)
+
+    def frame(self, i: int) -> "NativeScheme":
+        """rt_scheme_frame: animation frame i as a still scheme."""
+        p = C.c_void_p()
+        st = self.lib.rt_scheme_frame(self.ptr, int(i), C.byref(p))
+        if st != abi.RT_OK:
+            raise abi.RtError(st, (self.lib.rt_scheme_last_error() or b"").decode())
+        return NativeScheme._wrap(self.lib, p)
+
     def close(self):
         if self.ptr:
             self.lib.rt_scheme_free(self.ptr)

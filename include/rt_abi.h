@@ -307,6 +307,13 @@ int         rt_scheme_load(const char* text, uint64_t len, uint32_t format, cons
                            uint64_t seed, rt_scheme** out);
 int         rt_scheme_view_get(rt_scheme* scheme, rt_scheme_view* out);
 const char* rt_scheme_last_error(void);   /* this thread's last rt_scheme_load failure */
+
+/* Animation (renderer.rs:65-207, builder/inner.rs:113-249): the number of frames of an
+ * animated scheme (0 when render_info.animation is off), and frame i as a still scheme whose
+ * spheres / models sit at their keyframe-interpolated places (free with rt_scheme_free).  The
+ * keyframe crate's easing is restated, not pinned. */
+int         rt_scheme_frames(rt_scheme* scheme, uint32_t* n_frames);
+int         rt_scheme_frame(rt_scheme* scheme, uint32_t frame, rt_scheme** out);
 int         rt_scheme_free(rt_scheme* scheme);
 
 /* process_output_routine (ui_util.rs:37-54): an RGBA8 buffer (width*height*4, row y = pixel

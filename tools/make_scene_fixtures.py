@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
 from rt_amd import scheme  # noqa: E402
 
 REF = "/root/reference/schemes"
-NAMES = ["walled", "triangles", "biplane", "spaceship_r1", "a380", "outside_spheres"]
+NAMES = ["walled", "triangles", "biplane", "spaceship_r1", "a380", "outside_spheres", "bounce_anim", "biplane_anim"]
 
 if __name__ == "__main__":
     out_dir = os.path.join(ROOT, "tests", "golden", "scenes")
