@@ -42,6 +42,7 @@ struct rt_ctx {
     float* radiance = nullptr;    // K > 1 sample buffer
     uint64_t radiance_cap = 0;    // floats
     uint64_t lane_capacity = 0;   // lanes resident at the kernel's occupancy
+    uint32_t n_cu = 0;
     uint32_t forced_k = 0;        // RT_LANES_PER_PIXEL (tests / tuning)
     uint32_t* d_queue = nullptr;  // queue schedule item counter
     int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
@@ -344,6 +345,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     hipDeviceProp_t prop;
     HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
     c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
+    c->n_cu = (uint32_t)prop.multiProcessorCount;
     if (hipMalloc(&c->d_queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
     if (const char* e = std::getenv("RT_SCHED")) {
         if (!std::strcmp(e, "direct")) c->sched = 1;
@@ -489,7 +491,10 @@ static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64
         uint64_t chunk = QUEUE_RADIANCE_FLOATS / (3 * n_out);
         if (chunk < 1) chunk = 1;
         if (chunk > sample_count) chunk = sample_count ? sample_count : 1;
-        const uint64_t lanes = c->lane_capacity;
+        int per_cu = 0;  // the queue grid: the resident workgroups of this scene's kernel
+        HIPCHK(c, queue_blocks_per_cu(a, &per_cu));
+        if (per_cu < 1) per_cu = 1;
+        const uint64_t lanes = (uint64_t)c->n_cu * (uint64_t)per_cu * BLOCK;
         // the counter overshoots n_items by at most one grab (<= 1024 = 16 x 64) per wave
         if ((uint64_t)n_out * chunk + lanes * 16 >= (1ull << 32)) chunk = ((1ull << 32) - lanes * 16 - 1) / n_out;
         if (chunk < 1) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels for one launch");

@@ -145,5 +145,6 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_fold(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s);
+hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks);
 
 }  // namespace rtd

@@ -49,6 +49,9 @@
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
+#ifndef RT_MIN_WAVES_GEN
+#define RT_MIN_WAVES_GEN RT_MIN_WAVES  // the same for the general (triangle / mesh) kernels
+#endif
 #ifndef RT_LDS_SPHERES
 #define RT_LDS_SPHERES 64   // 1 KiB
 #endif
@@ -934,11 +937,13 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
 #endif
 #if RT_LDS_SPHERES > 0
-    k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+    if (!GEN) {  // only the sphere-only kernel reads the LDS sphere table
+        k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+        for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+    }
 #endif
 #if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
-    __syncthreads();
+    if (!GEN || RT_LDS_NODES > 0) __syncthreads();
 #endif
 
     // workgroup -> tile -> block of 16 x (8/K) pixels, K lanes per pixel (adjacent lanes)
@@ -1034,7 +1039,7 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
 
 template <bool GEN, bool DLS = false>
 #if RT_MIN_WAVES > 0
-__global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
 #else
 __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
 #endif
@@ -1046,11 +1051,13 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
 #endif
 #if RT_LDS_SPHERES > 0
-    k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+    if (!GEN) {  // only the sphere-only kernel reads the LDS sphere table
+        k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+        for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+    }
 #endif
 #if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
-    __syncthreads();
+    if (!GEN || RT_LDS_NODES > 0) __syncthreads();
 #endif
     uint32_t* st = dyn_lds + threadIdx.x;
     Ctr<false> c;
@@ -1149,6 +1156,15 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((trace_kernel<false, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
+// Resident workgroups per CU of the queue kernel this scene launches (its registers and LDS
+// stack decide): the queue grid is exactly that many workgroups per CU.
+hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks) {
+    const size_t lds = stack_lds_bytes(a);
+    if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true, true>, BLOCK, lds);
+    if (a.sc.spheres_only) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true>, BLOCK, lds);
+}
+
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
     if (a.sc.dls)
         hipLaunchKernelGGL((queue_kernel<true, true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
