@@ -43,6 +43,9 @@
 #ifndef RT_LEAF2
 #define RT_LEAF2 2          // general leaves: refs per step, all their loads issued first (1: plain loop)
 #endif
+#ifndef RT_COOP
+#define RT_COOP 1           // general queue kernel: the wave tests its lanes' leaf refs cooperatively
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -593,6 +596,163 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, cons
     return false;
 }
 
+// ------------------------------------------------------------ cooperative leaf tests (meshes)
+// With one lane per ray, a wave tests leaf refs for as long as its *longest* leaf: mesh leaves
+// average ~23 refs and the longest of 64 is ~4x that, so 3/4 of the lanes idle (biplane: 24%
+// VALU lane utilisation).  Here every lane of the wave reaches its next leaf, then the wave
+// tests all their (ray, ref) pairs as one list, 64 at a time: a pair's owner comes from a
+// binary search over the wave's inclusive prefix of leaf sizes, and the owner's ray and leaf
+// are read with cross-lane shuffles.  Each owner's leaf minimum is an LDS atomicMin on
+// (bits(l) << 32 | position in the leaf): positive floats order like their bit patterns, so this
+// is the first strict minimum in leaf order (closest_hit.rs:25), exactly; NaN lengths never
+// win (see leaf_closest).  The owner then re-tests the winning ref for its barycentrics.
+#if RT_COOP
+__shared__ unsigned long long g_coop_key[BLOCK];
+#endif
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d);
+        v += lane >= d ? u : 0u;
+    }
+    return v;
+}
+
+// Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
+__device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
+                                                        uint32_t cnt, uint32_t lane) {
+#if RT_COOP
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t total = __shfl(incl, 63);
+    const uint32_t wbase = threadIdx.x & ~63u;
+    g_coop_key[threadIdx.x] = ~0ull;
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t w = base + lane;
+        uint32_t owner = 0;  // lanes whose inclusive end is <= w
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+            const uint32_t e = __shfl(incl, owner + step - 1);
+            owner += e <= w ? step : 0u;
+        }
+        const uint32_t o_end = __shfl(incl, owner), o_cnt = __shfl(cnt, owner), o_off = __shfl(off, owner);
+        Ray ro;
+        ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+        ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+        if (w < total) {
+            const uint32_t pos = w - (o_end - o_cnt);
+            const uint32_t ref = sc.refs[o_off + pos];
+            const float4* pd = prim_data(sc, ref);
+            float l = 0.f, bu, bv;
+            bool h;
+            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(pd[0], ro, &l);
+            else h = tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), ro, &l, &bu, &bv);
+            if (h && l >= HIT_MIN)  // valid and not NaN
+                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | pos);
+        }
+    }
+    return g_coop_key[threadIdx.x];
+#else
+    (void)sc; (void)r; (void)off; (void)cnt; (void)lane;
+    return ~0ull;
+#endif
+}
+
+// stack_search with cooperative leaves: the same per-lane traversal (kdtree.rs:66-104); lanes
+// whose search has ended (or that had no ray) keep looping as helpers until the wave is done.
+template <bool FAST>
+__device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
+                                                  bool active, float root_entry, float root_exit, Hit* best,
+                                                  uint32_t* st) {
+    float entry = root_entry, exit_t = root_exit, top_t = root_exit;
+    uint32_t node = 0;
+    int sp = 0;
+    bool done = !active, found = false;
+    const uint32_t lane = __lane_id();
+    while (__ballot(!done) != 0) {
+        uint32_t off = 0, cnt = 0;
+        if (!done) {
+            uint2 nd = fetch_node(sc, k, node);
+            while ((nd.y & 3u) != RT_KD_LEAF) {
+                float d;
+                const float t = split_t<FAST>(nd, ax, r, &d);
+                const bool pos = d > 0.0f;
+                const bool go_near = t >= exit_t;
+                const bool go_far = !go_near && t <= entry;
+                const bool push = !go_near && !go_far;
+                st[sp * BLOCK] = node;
+                sp += push ? 1 : 0;
+                top_t = push ? t : top_t;
+                exit_t = push ? t : exit_t;
+                node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
+                nd = fetch_node(sc, k, node);
+            }
+            off = nd.y >> 2;
+            cnt = nd.x;
+        }
+        const unsigned long long key = coop_leaf(sc, r, off, cnt, lane);
+        if (!done) {
+            bool ret = false;
+            if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
+                const uint32_t ref = sc.refs[off + (uint32_t)key];
+                const float4* pd = prim_data(sc, ref);
+                float l = 0.f, bu = 0.f, bv = 0.f;
+                if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(pd[0], r, &l);
+                else (void)tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), r, &l, &bu, &bv);
+                best->ref = ref;
+                best->l = l;
+                best->bu = bu;
+                best->bv = bv;
+                ret = l <= exit_t + EPS;
+            }
+            if (ret) {
+                done = true;
+                found = true;
+            } else if (sp == 0) {
+                done = true;
+            } else {
+                --sp;
+                const uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
+                float d;
+                (void)split_t<FAST>(pn, ax, r, &d);
+                node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
+                entry = top_t;
+                if (sp) {
+                    top_t = split_t<FAST>(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
+                    exit_t = top_t;
+                } else {
+                    exit_t = root_exit;
+                }
+            }
+        }
+    }
+    return found;
+}
+
+// closest() for the general queue kernel: called by every lane of the wave; `active` lanes
+// have a ray.
+__device__ __forceinline__ bool closest_coop(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
+                                             uint32_t* st, bool active) {
+    float root_entry = 0.f, root_exit = 0.f;
+    const RayAx ax = ray_axes(r);
+    const bool in = active && sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit);
+    bool found;
+#if RT_FASTDIV
+    const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
+    if (__builtin_expect(__ballot(!fast) == 0, 1))
+        found = stack_search_coop<true>(sc, k, r, ax, in, root_entry, root_exit, best, st);
+    else
+#endif
+        found = stack_search_coop<false>(sc, k, r, ax, in, root_entry, root_exit, best, st);
+    if (found) return true;
+    if (active && sc.has_cube) {
+        best->ref = REF_CUBE;
+        best->l = __builtin_inff();
+        return true;
+    }
+    return false;
+}
+
 // ---------------------------------------------------------------- materials (interaction.rs)
 __device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rng); }
 
@@ -839,12 +999,13 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
 
 // Traces one segment of `p`.  Returns true when the path has ended (miss, cube map, Russian
 // roulette, debug_single_ray, bounce cap); p.L then holds the sample's radiance.
-template <bool COUNT, bool GEN, bool DLS = false>
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
-                                        Ctr<COUNT>& c) {
+                                        Ctr<COUNT>& c, bool active = true) {
     if (COUNT) c.segments++;
     Hit h;
-    const bool hit = closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
+    const bool hit = COOP ? closest_coop(sc, k, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
+    if (COOP && !active) return false;
     if (DLS && p.dls_on) {  // the previous vertex's DLS term, now that its continued ray has hit
         p.L = p.L + cmul(p.dls_T, dls_contrib(sc, p, hit ? h.ref : REF_NONE));
         p.dls_on = false;
@@ -1105,7 +1266,10 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
             }
         }
         if (__ballot(have) == 0) break;
-        if (have && segment<false, GEN, DLS>(sc, k, p, st, c)) {
+        // the cooperative traversal needs every lane of the wave: lanes without a path help
+        const bool fin = (GEN && RT_COOP) ? segment<false, GEN, DLS, GEN && RT_COOP>(sc, k, p, st, c, have) && have
+                                          : have && segment<false, GEN, DLS>(sc, k, p, st, c);
+        if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;
             r[1] = p.L.y;
