@@ -46,6 +46,12 @@
 #ifndef RT_COOP
 #define RT_COOP 1           // general queue kernel: the wave tests its lanes' leaf refs cooperatively
 #endif
+#ifndef RT_COOP_ITEMS
+#define RT_COOP_ITEMS 1     // cooperative leaves: (ray, ref) pairs per lane per pass (1 or 2)
+#endif
+#ifndef RT_COOP_DESC
+#define RT_COOP_DESC 0      // cooperative traversal: node steps per lane per round (0: to the leaf)
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -627,8 +633,13 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
     g_coop_key[threadIdx.x] = ~0ull;
-    for (uint32_t base = 0; base < total; base += 64) {
-        const uint32_t w = base + lane;
+    struct Item {
+        bool ok;
+        uint32_t owner, pos, ref;
+        Ray ro;
+        float4 d0, d1, d2;
+    };
+    auto fetch = [&](uint32_t w, Item& it) {
         uint32_t owner = 0;  // lanes whose inclusive end is <= w
 #pragma unroll
         for (uint32_t step = 32; step; step >>= 1) {
@@ -636,20 +647,39 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             owner += e <= w ? step : 0u;
         }
         const uint32_t o_end = __shfl(incl, owner), o_cnt = __shfl(cnt, owner), o_off = __shfl(off, owner);
-        Ray ro;
-        ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
-        ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
-        if (w < total) {
-            const uint32_t pos = w - (o_end - o_cnt);
-            const uint32_t ref = sc.refs[o_off + pos];
-            const float4* pd = prim_data(sc, ref);
-            float l = 0.f, bu, bv;
-            bool h;
-            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(pd[0], ro, &l);
-            else h = tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), ro, &l, &bu, &bv);
-            if (h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | pos);
+        it.ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+        it.ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+        it.owner = owner;
+        it.ok = w < total;
+        it.pos = w - (o_end - o_cnt);
+        it.ref = it.ok ? sc.refs[o_off + it.pos] : 0u;
+        const float4* pd = prim_data(sc, it.ref);
+        if (it.ok) {
+            it.d0 = pd[0];
+            it.d1 = pd[1];
+            it.d2 = pd[2];
         }
+    };
+    auto test = [&](const Item& it) {
+        if (!it.ok) return;
+        float l = 0.f, bu, bv;
+        bool h;
+        if (__builtin_expect((it.ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(it.d0, it.ro, &l);
+        else h = tri_hit(xyz(it.d0), xyz(it.d1), xyz(it.d2), it.ro, &l, &bu, &bv);
+        if (h && l >= HIT_MIN)  // valid and not NaN
+            atomicMin(&g_coop_key[wbase + it.owner], ((unsigned long long)__float_as_uint(l) << 32) | it.pos);
+    };
+    for (uint32_t base = 0; base < total; base += 64 * RT_COOP_ITEMS) {
+        Item a;
+        fetch(base + lane, a);
+#if RT_COOP_ITEMS > 1
+        Item b;
+        fetch(base + 64 + lane, b);
+#endif
+        test(a);
+#if RT_COOP_ITEMS > 1
+        test(b);
+#endif
     }
     return g_coop_key[threadIdx.x];
 #else
@@ -671,9 +701,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
     const uint32_t lane = __lane_id();
     while (__ballot(!done) != 0) {
         uint32_t off = 0, cnt = 0;
+        bool at_leaf = false;
         if (!done) {
             uint2 nd = fetch_node(sc, k, node);
-            while ((nd.y & 3u) != RT_KD_LEAF) {
+            uint32_t steps = 0;
+            while ((nd.y & 3u) != RT_KD_LEAF && (RT_COOP_DESC == 0 || steps < RT_COOP_DESC)) {
+                ++steps;
                 float d;
                 const float t = split_t<FAST>(nd, ax, r, &d);
                 const bool pos = d > 0.0f;
@@ -687,11 +720,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
                 node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
                 nd = fetch_node(sc, k, node);
             }
-            off = nd.y >> 2;
-            cnt = nd.x;
+            at_leaf = (nd.y & 3u) == RT_KD_LEAF;
+            off = at_leaf ? nd.y >> 2 : 0u;
+            cnt = at_leaf ? nd.x : 0u;
         }
         const unsigned long long key = coop_leaf(sc, r, off, cnt, lane);
-        if (!done) {
+        if (!done && at_leaf) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
                 const uint32_t ref = sc.refs[off + (uint32_t)key];
