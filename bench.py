@@ -216,7 +216,7 @@ def main():
                            "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2, gfx950)",
                            "traffic_source": traffic[1] if traffic else None,
                            "algorithmic_bytes_per_launch": round(bps * per_launch),
-                           "kernel": f"rtd::queue_kernel<{'false' if spheres_only else 'true'}>",
+                           "kernel": f"rtd::queue_kernel<{'false' if spheres_only else 'true'}, {'true' if int(loaded.info.dir_light_samp) else 'false'}>",
                            "kernel_ms_avg": round(avg_ms, 3), "launches_per_step": n_launch / args.steps,
                            "step_device_ms_avg": round(sum(kernel_ms) / len(kernel_ms), 3),
                            "bytes_per_sample": round(bps, 1), "traversal_bytes_per_sample": round(trav_bps, 1),
