@@ -46,11 +46,8 @@
 #ifndef RT_COOP
 #define RT_COOP 1           // general queue kernel: the wave tests its lanes' leaf refs cooperatively
 #endif
-#ifndef RT_COOP_ITEMS
-#define RT_COOP_ITEMS 1     // cooperative leaves: (ray, ref) pairs per lane per pass (1 or 2)
-#endif
-#ifndef RT_COOP_DESC
-#define RT_COOP_DESC 0      // cooperative traversal: node steps per lane per round (0: to the leaf)
+#ifndef RT_MERGED
+#define RT_MERGED 0         // general queue kernel: one loop of traversal rounds (merged_kernel)
 #endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
@@ -633,13 +630,8 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
     g_coop_key[threadIdx.x] = ~0ull;
-    struct Item {
-        bool ok;
-        uint32_t owner, pos, ref;
-        Ray ro;
-        float4 d0, d1, d2;
-    };
-    auto fetch = [&](uint32_t w, Item& it) {
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t w = base + lane;
         uint32_t owner = 0;  // lanes whose inclusive end is <= w
 #pragma unroll
         for (uint32_t step = 32; step; step >>= 1) {
@@ -647,39 +639,20 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             owner += e <= w ? step : 0u;
         }
         const uint32_t o_end = __shfl(incl, owner), o_cnt = __shfl(cnt, owner), o_off = __shfl(off, owner);
-        it.ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
-        it.ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
-        it.owner = owner;
-        it.ok = w < total;
-        it.pos = w - (o_end - o_cnt);
-        it.ref = it.ok ? sc.refs[o_off + it.pos] : 0u;
-        const float4* pd = prim_data(sc, it.ref);
-        if (it.ok) {
-            it.d0 = pd[0];
-            it.d1 = pd[1];
-            it.d2 = pd[2];
+        Ray ro;
+        ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+        ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+        if (w < total) {
+            const uint32_t pos = w - (o_end - o_cnt);
+            const uint32_t ref = sc.refs[o_off + pos];
+            const float4* pd = prim_data(sc, ref);
+            float l = 0.f, bu, bv;
+            bool h;
+            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(pd[0], ro, &l);
+            else h = tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), ro, &l, &bu, &bv);
+            if (h && l >= HIT_MIN)  // valid and not NaN
+                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | pos);
         }
-    };
-    auto test = [&](const Item& it) {
-        if (!it.ok) return;
-        float l = 0.f, bu, bv;
-        bool h;
-        if (__builtin_expect((it.ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(it.d0, it.ro, &l);
-        else h = tri_hit(xyz(it.d0), xyz(it.d1), xyz(it.d2), it.ro, &l, &bu, &bv);
-        if (h && l >= HIT_MIN)  // valid and not NaN
-            atomicMin(&g_coop_key[wbase + it.owner], ((unsigned long long)__float_as_uint(l) << 32) | it.pos);
-    };
-    for (uint32_t base = 0; base < total; base += 64 * RT_COOP_ITEMS) {
-        Item a;
-        fetch(base + lane, a);
-#if RT_COOP_ITEMS > 1
-        Item b;
-        fetch(base + 64 + lane, b);
-#endif
-        test(a);
-#if RT_COOP_ITEMS > 1
-        test(b);
-#endif
     }
     return g_coop_key[threadIdx.x];
 #else
@@ -701,12 +674,9 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
     const uint32_t lane = __lane_id();
     while (__ballot(!done) != 0) {
         uint32_t off = 0, cnt = 0;
-        bool at_leaf = false;
         if (!done) {
             uint2 nd = fetch_node(sc, k, node);
-            uint32_t steps = 0;
-            while ((nd.y & 3u) != RT_KD_LEAF && (RT_COOP_DESC == 0 || steps < RT_COOP_DESC)) {
-                ++steps;
+            while ((nd.y & 3u) != RT_KD_LEAF) {
                 float d;
                 const float t = split_t<FAST>(nd, ax, r, &d);
                 const bool pos = d > 0.0f;
@@ -720,12 +690,11 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
                 node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
                 nd = fetch_node(sc, k, node);
             }
-            at_leaf = (nd.y & 3u) == RT_KD_LEAF;
-            off = at_leaf ? nd.y >> 2 : 0u;
-            cnt = at_leaf ? nd.x : 0u;
+            off = nd.y >> 2;
+            cnt = nd.x;
         }
         const unsigned long long key = coop_leaf(sc, r, off, cnt, lane);
-        if (!done && at_leaf) {
+        if (!done) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
                 const uint32_t ref = sc.refs[off + (uint32_t)key];
@@ -1033,13 +1002,10 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
 
 // Traces one segment of `p`.  Returns true when the path has ended (miss, cube map, Russian
 // roulette, debug_single_ray, bounce cap); p.L then holds the sample's radiance.
-template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false>
-__device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
-                                        Ctr<COUNT>& c, bool active = true) {
-    if (COUNT) c.segments++;
-    Hit h;
-    const bool hit = COOP ? closest_coop(sc, k, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
-    if (COOP && !active) return false;
+// Everything of a segment after its closest hit: hit_info, emission, Russian roulette and the
+// continued ray.  Returns true when the path has ended.
+template <bool COUNT, bool GEN, bool DLS>
+__device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& p, Hit h, bool hit, Ctr<COUNT>& c) {
     if (DLS && p.dls_on) {  // the previous vertex's DLS term, now that its continued ray has hit
         p.L = p.L + cmul(p.dls_T, dls_contrib(sc, p, hit ? h.ref : REF_NONE));
         p.dls_on = false;
@@ -1099,6 +1065,16 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
         p.dls_T = p.T;
     }
     return ++p.depth >= MAX_BOUNCES;
+}
+
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false>
+__device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
+                                        Ctr<COUNT>& c, bool active = true) {
+    if (COUNT) c.segments++;
+    Hit h;
+    const bool hit = COOP ? closest_coop(sc, k, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
+    if (COOP && !active) return false;
+    return shade<COUNT, GEN, DLS>(sc, k, p, h, hit, c);
 }
 
 __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, int y, uint32_t pix,
@@ -1313,6 +1289,184 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ merged traversal loop
+// queue_kernel<true> with RT_COOP ends a segment's traversal when the wave's slowest ray does:
+// lanes that resolved early only help with leaf passes.  Here the loop *is* the traversal: every
+// round each lane descends to its next leaf, the wave tests the leaves cooperatively, and a lane
+// whose traversal resolved shades at once and starts its next ray (or takes a new item) in the
+// next round.  Same per-ray semantics as stack_search (kdtree.rs:66-104).
+template <bool FAST>
+__device__ __forceinline__ void descend_step_loop(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
+                                                  uint32_t& node, int& sp, float& entry, float& exit_t,
+                                                  float& top_t, uint32_t* st, uint2& nd) {
+    nd = fetch_node(sc, k, node);
+    while ((nd.y & 3u) != RT_KD_LEAF) {
+        float d;
+        const float t = split_t<FAST>(nd, ax, r, &d);
+        const bool pos = d > 0.0f;
+        const bool go_near = t >= exit_t;
+        const bool go_far = !go_near && t <= entry;
+        const bool push = !go_near && !go_far;
+        st[sp * BLOCK] = node;
+        sp += push ? 1 : 0;
+        top_t = push ? t : top_t;
+        exit_t = push ? t : exit_t;
+        node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
+        nd = fetch_node(sc, k, node);
+    }
+}
+template <bool FAST>
+__device__ __forceinline__ void pop_far(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
+                                        uint32_t& node, int& sp, float& entry, float& exit_t, float& top_t,
+                                        float root_exit, uint32_t* st) {
+    --sp;
+    const uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
+    float d;
+    (void)split_t<FAST>(pn, ax, r, &d);
+    node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
+    entry = top_t;
+    if (sp) {
+        top_t = split_t<FAST>(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
+        exit_t = top_t;
+    } else {
+        exit_t = root_exit;
+    }
+}
+
+template <bool DLS>
+#if RT_MIN_WAVES > 0
+__global__ __launch_bounds__(BLOCK, RT_MIN_WAVES_GEN) void merged_kernel(LaunchArgs a) {
+#else
+__global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
+#endif
+    extern __shared__ uint32_t dyn_lds[];
+    const DevScene& sc = a.sc;
+    const Cache k{0, 0};
+    uint32_t* st = dyn_lds + threadIdx.x;
+    Ctr<false> c;
+    const uint32_t lane = __lane_id();
+    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    uint32_t pool = 0, pool_end = 0, grab = grab_size(a.n_items, n_waves);
+    bool have = false, qdone = false, need = false, tr = false;
+    uint32_t slot = 0, node = 0;
+    int sp = 0;
+    float entry = 0.f, exit_t = 0.f, top_t = 0.f, root_exit = 0.f;
+    Path p;
+    for (;;) {
+        const uint64_t want = __ballot(!have && !qdone);
+        if (want) {
+            const uint32_t n = (uint32_t)__popcll(want);
+            const uint32_t left = pool_end - pool;
+            uint32_t base = pool_end;
+            if (left < n) {
+                uint32_t b0 = 0;
+                const uint32_t first = (uint32_t)__ffsll((unsigned long long)want) - 1u;
+                if (lane == first) b0 = atomicAdd(a.queue, grab);
+                base = __builtin_amdgcn_readfirstlane(__shfl(b0, first));
+            }
+            if (!have && !qdone) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+                const uint32_t item = rk < left ? pool + rk : base + (rk - left);
+                if (item < a.n_items) {
+                    const uint32_t j = item / a.n_pix, o = item - j * a.n_pix;
+                    const DevTile tl = a.tiles[tile_of(a, o)];
+                    const uint32_t lo = o - tl.out_off;
+                    const int x = (int)(tl.x0 + lo % tl.w), y = (int)(tl.y0 + lo / tl.w);
+                    start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
+                    slot = item;
+                    have = true;
+                    need = true;
+                } else {
+                    qdone = true;
+                }
+            }
+            if (left < n) {
+                pool = base + (n - left);
+                pool_end = base + grab;
+                grab = grab_size(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+            } else {
+                pool += n;
+            }
+        }
+        if (__ballot(have) == 0) break;
+
+        bool resolved = false, hit = false;
+        Hit h;
+        const RayAx ax = ray_axes(p.ray);
+        if (need) {  // a new traversal: root slab test (kdtree.rs:59-61)
+            need = false;
+            float re = 0.f, rx = 0.f;
+            if (sc.n_nodes && entry_exit(sc.bounds, ax, p.ray, &re, &rx)) {
+                tr = true;
+                node = 0;
+                sp = 0;
+                entry = re;
+                exit_t = top_t = root_exit = rx;
+            } else {
+                resolved = true;
+            }
+        }
+        bool fastw = true;
+#if RT_FASTDIV
+        fastw = __ballot(tr && !(sc.fastdiv && origin_fast_ok(p.ray.o))) == 0;
+#else
+        fastw = false;
+#endif
+        uint32_t off = 0, cnt = 0;
+        if (tr) {
+            uint2 nd;
+            if (fastw) descend_step_loop<true>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, st, nd);
+            else descend_step_loop<false>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, st, nd);
+            off = nd.y >> 2;
+            cnt = nd.x;
+        }
+        const unsigned long long key = coop_leaf(sc, p.ray, off, cnt, lane);
+        if (tr) {
+            bool ret = false;
+            if (key != ~0ull) {
+                const uint32_t ref = sc.refs[off + (uint32_t)key];
+                const float4* pd = prim_data(sc, ref);
+                float l = 0.f, bu = 0.f, bv = 0.f;
+                if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(pd[0], p.ray, &l);
+                else (void)tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), p.ray, &l, &bu, &bv);
+                h.ref = ref;
+                h.l = l;
+                h.bu = bu;
+                h.bv = bv;
+                ret = l <= exit_t + EPS;
+            }
+            if (ret) {
+                tr = false;
+                resolved = hit = true;
+            } else if (sp == 0) {
+                tr = false;
+                resolved = true;
+            } else if (fastw) {
+                pop_far<true>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, root_exit, st);
+            } else {
+                pop_far<false>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, root_exit, st);
+            }
+        }
+        if (resolved) {
+            if (!hit && sc.has_cube) {  // unconditional renderables (kdtree.rs:61,103)
+                h.ref = REF_CUBE;
+                h.l = __builtin_inff();
+                hit = true;
+            }
+            if (shade<false, true, DLS>(sc, k, p, h, hit, c)) {
+                float* rr = a.radiance + 3 * (size_t)slot;
+                rr[0] = p.L.x;
+                rr[1] = p.L.y;
+                rr[2] = p.L.z;
+                have = false;
+            } else {
+                need = true;
+            }
+        }
+    }
+}
+
 // Running mean over the traced chunk, in sample order (draw_scene.rs:81-83): one lane per
 // launch pixel; reads are coalesced across lanes ([sample][pixel] layout).
 __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
@@ -1358,12 +1512,27 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
 // stack decide): the queue grid is exactly that many workgroups per CU.
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks) {
     const size_t lds = stack_lds_bytes(a);
+#if RT_MERGED && RT_COOP
+    if (!a.sc.spheres_only) {
+        if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, merged_kernel<true>, BLOCK, lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, merged_kernel<false>, BLOCK, lds);
+    }
+#endif
     if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true, true>, BLOCK, lds);
     if (a.sc.spheres_only) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, lds);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true>, BLOCK, lds);
 }
 
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
+#if RT_MERGED && RT_COOP
+    if (!a.sc.spheres_only) {
+        if (a.sc.dls)
+            hipLaunchKernelGGL((merged_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+        else
+            hipLaunchKernelGGL((merged_kernel<false>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+        return hipGetLastError();
+    }
+#endif
     if (a.sc.dls)
         hipLaunchKernelGGL((queue_kernel<true, true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else if (a.sc.spheres_only)
