@@ -49,6 +49,9 @@
 #ifndef RT_MERGED
 #define RT_MERGED 0         // general queue kernel: one loop of traversal rounds (merged_kernel)
 #endif
+#ifndef RT_DPP_SCAN
+#define RT_DPP_SCAN 1       // wave prefix sums by DPP row shifts / broadcasts (else ds_bpermute)
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -613,13 +616,28 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, cons
 __shared__ unsigned long long g_coop_key[BLOCK];
 #endif
 
+// Inclusive prefix sum over the 64 lanes.  DPP (GFX9): row_shr 1/2/4/8 with bound control
+// (lanes shifted in from outside the 16-lane row read 0) scans each row; row_bcast:15 adds row
+// r's total to row r+1 for rows 1 and 3, row_bcast:31 adds rows 0-1's total to rows 2-3.  No
+// LDS, no per-lane address registers (the ds_bpermute form kept six of them live).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#if RT_DPP_SCAN
+    (void)lane;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+#else
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
         const uint32_t u = __shfl_up(v, d);
         v += lane >= d ? u : 0u;
     }
     return v;
+#endif
 }
 
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
