@@ -52,6 +52,9 @@
 #ifndef RT_DPP_SCAN
 #define RT_DPP_SCAN 1       // wave prefix sums by DPP row shifts / broadcasts (else ds_bpermute)
 #endif
+#ifndef RT_OWNER_SCAN
+#define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -614,7 +617,19 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, cons
 // win (see leaf_closest).  The owner then re-tests the winning ref for its barycentrics.
 #if RT_COOP
 __shared__ unsigned long long g_coop_key[BLOCK];
+__shared__ uint32_t g_coop_slot[BLOCK];
 #endif
+
+// Inclusive prefix maximum over the 64 lanes (the DPP pattern of wave_incl_scan with max).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
 
 // Inclusive prefix sum over the 64 lanes.  DPP (GFX9): row_shr 1/2/4/8 with bound control
 // (lanes shifted in from outside the 16-lane row read 0) scans each row; row_bcast:15 adds row
@@ -647,15 +662,33 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
-    g_coop_key[threadIdx.x] = ~0ull;
+    __hip_atomic_store(&g_coop_key[threadIdx.x], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t w = base + lane;
+#if RT_OWNER_SCAN
+        // The owner of item w is the first lane whose inclusive end exceeds w.  The pass's first
+        // item's owner is the count of lanes ending at or before it (one ballot); every other
+        // owner starting inside the pass marks its start slot; a prefix maximum over the slots
+                // gives each lane its owner (+1).  Owners with items have distinct starts: no collision.
+        // (relaxed wavefront-scope atomics: lanes talk through LDS, and a plain access would let
+        // the compiler forward a lane's own store to its read, missing the other lanes' writes)
+        const uint32_t first = (uint32_t)__popcll(__ballot(incl <= base));
+        __hip_atomic_store(&g_coop_slot[threadIdx.x], lane == 0 ? first + 1u : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t start = incl - cnt;
+        if (cnt && start > base && start < base + 64u)
+            __hip_atomic_store(&g_coop_slot[wbase + (start - base)], lane + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t owner =
+            wave_incl_max(__hip_atomic_load(&g_coop_slot[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) - 1u;
+#else
         uint32_t owner = 0;  // lanes whose inclusive end is <= w
 #pragma unroll
         for (uint32_t step = 32; step; step >>= 1) {
             const uint32_t e = __shfl(incl, owner + step - 1);
             owner += e <= w ? step : 0u;
         }
+#endif
         const uint32_t o_end = __shfl(incl, owner), o_cnt = __shfl(cnt, owner), o_off = __shfl(off, owner);
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
@@ -672,7 +705,7 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | pos);
         }
     }
-    return g_coop_key[threadIdx.x];
+    return __hip_atomic_load(&g_coop_key[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 #else
     (void)sc; (void)r; (void)off; (void)cnt; (void)lane;
     return ~0ull;
