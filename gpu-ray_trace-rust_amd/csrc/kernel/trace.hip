@@ -129,6 +129,24 @@ __device__ __forceinline__ V3 div3(V3 a, float b) {
     if (__builtin_expect(!(mk_range(b) && mk_num(a.x) && mk_num(a.y) && mk_num(a.z)), 0)) q = a / b;
     return q;
 }
+// sqrtf(x), bit for bit: v_sqrt_f32 and the +-1 ulp FMA correction of hipcc's IEEE sequence,
+// without its tiny-input scaling and class check — equal to sqrtf for x in {-0, +0} and every
+// x in [2^-80, +inf] (exhaustive, tools/check_exact_ops.hip; below 2^-80 it is not).
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    return fmaf(-su, s, x) > 0.0f ? su : r;
+}
+// sqrtf(x) for x = fmaxf(y, 0) (never NaN, never below -0).  bits - 1 wraps for +0 and is
+// >= 0x7fffffff for -0, so one compare sends exactly (0, 2^-80) to sqrtf — a divergent branch
+// no lane normally takes.
+__device__ __forceinline__ float sqrt_nonneg(float x) {
+    if (!RT_EXACT_FAST) return sqrtf(x);
+    float s = sqrt_rn(x);
+    if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
+    return s;
+}
 __device__ __forceinline__ V3 normalize(V3 a) {
     float n = sqrtf(dot(a, a));
     return div3(a, n);
@@ -199,9 +217,18 @@ __device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, const Cache& 
     return sc.sph[i];
 }
 
+#if RT_LDS_SPHERES > 0
+__device__ __forceinline__ void fill_lds_spheres(const DevScene& sc, Cache& k) {
+    k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+}
+#endif
+
 // ---------------------------------------------------------------- primitives
 // Sphere::intersect (sphere.rs:83-105)
-// Branch-free: sqrt of max(thing2, 0) equals sqrt(thing2) whenever the hit is taken.
+// Branch-free: sqrt of max(thing2, 0) equals sqrt(thing2) whenever the hit is taken.  With p0
+// and p1 both true neither root is NaN or zero, so a compare-select is fminf (without its NaN
+// canonicalisation).
 __device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
     const V3 oc = r.o - xyz(s);
     const float dir = dot(r.d, oc);
@@ -209,10 +236,10 @@ __device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
     const float thing2 = dir * dir - consts;
     const bool disc = thing2 > 0.0f;
     const float offset = -dir;
-    const float thing = sqrtf(fmaxf(thing2, 0.0f));
+    const float thing = sqrt_nonneg(fmaxf(thing2, 0.0f));
     const float l0 = offset + thing, l1 = offset - thing;
     const bool p0 = l0 > 0.0f, p1 = l1 > 0.0f;
-    *l = p0 ? (p1 ? fminf(l0, l1) : l0) : l1;  // filter(>0).reduce(min), sphere.rs:95
+    *l = p0 ? (p1 ? (l1 < l0 ? l1 : l0) : l0) : l1;  // filter(>0).reduce(min), sphere.rs:95
     return disc && (p0 || p1);
 }
 
@@ -265,8 +292,6 @@ __device__ __forceinline__ bool tri_hit_bf(V3 v0, V3 v1, V3 v2, const Ray& r, fl
 // Aabb::get_entry_exit (aabb.rs:22-62)
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
 // hits not shorter than 20*EPS.
-// SMALL: `mask` has bit i set iff sphere i has a valid hit (closest_small); other spheres
-// cannot be the leaf's candidate and are not re-tested.
 // Device data of a leaf ref: a sphere's float4 {c, r} or a triangle's three vertices.
 __device__ __forceinline__ const float4* prim_data(const DevScene& sc, uint32_t ref) {
     const uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
@@ -316,11 +341,11 @@ __device__ __forceinline__ void leaf_step(const LeafSlot& sl, const Ray& r, Hit*
 template <bool COUNT, bool GEN, bool SMALL = false>
 __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
                                              uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c,
-                                             uint32_t mask = 0, uint32_t imin = 0, float lmin = 0.f) {
+                                             uint32_t imin = 0, float lmin = 0.f) {
     if (SMALL && RT_LEAF_PMIN) {
         // If the leaf holds the globally closest sphere, that sphere is its candidate: no other
         // leaf sphere is closer, and on a tie the lowest renderable index wins both globally and
-        // in leaf order.  Only otherwise are the leaf's masked spheres re-tested.
+        // in leaf order.  Only otherwise are the leaf's spheres re-tested.
         bool has_min = false;
         for (uint32_t j = 0; j < cnt; ++j) has_min |= (sc.refs[off + j] & REF_INDEX_MASK) == imin;
         if (has_min) {
@@ -361,7 +386,6 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
     for (uint32_t j = 0; j < cnt; ++j) {
         uint32_t ref = sc.refs[off + j];
         uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
-        if (SMALL && !((mask >> idx) & 1u)) continue;
         float l = 0.f, bu = 0.f, bv = 0.f;
         bool h;
         if (!GEN || kind == K_SPHERE) {
@@ -482,8 +506,7 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
 template <bool COUNT, bool GEN, bool FAST, bool SMALL = false>
 __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
                                              float root_entry, float root_exit, Hit* best, uint32_t* st,
-                                             Ctr<COUNT>& c, uint32_t mask = 0, uint32_t imin = 0,
-                                             float lmin = 0.f) {
+                                             Ctr<COUNT>& c, uint32_t imin = 0, float lmin = 0.f) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0;
     int sp = 0;
@@ -505,7 +528,7 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
             nd = fetch_node(sc, k, node);
         }
         if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-        if (leaf_closest<COUNT, GEN, SMALL>(sc, k, nd.y >> 2, nd.x, r, best, c, mask, imin, lmin) &&
+        if (leaf_closest<COUNT, GEN, SMALL>(sc, k, nd.y >> 2, nd.x, r, best, c, imin, lmin) &&
             best->l <= exit_t + EPS)
             return true;
         if (sp == 0) return false;
@@ -533,27 +556,27 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
 // with fl(exit + EPS) < L* can never return.  Descending from entry E, where
 // fl(E + EPS) < L* holds for every value <= E, skips exactly such leaves (a near child whose
 // interval ends at or before E is not entered) and leaves every other leaf's interval, order
-// and exit untouched — so the returned sphere and distance are the reference's.  Leaves
-// only re-test spheres in the hit mask.  The instrumented (COUNT) kernel keeps the plain
-// traversal: its counters are the reference's work.
+// and exit untouched — so the returned sphere and distance are the reference's.  The
+// instrumented (COUNT) kernel keeps the plain traversal: its counters are the reference's work.
 template <bool COUNT>
 __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                               uint32_t* st, Ctr<COUNT>& c) {
-    uint32_t mask = 0, imin = 0;
+    uint32_t imin = 0;
+    bool any = false;
     float ls = __builtin_inff();
     if (COUNT) c.sph += sc.n_spheres;
 #pragma unroll RT_SPH_UNROLL
     for (uint32_t i = 0; i < sc.n_spheres; ++i) {
         float l;
         const bool v = sphere_hit(fetch_sphere<false>(sc, k, i), r, &l) & !(l < HIT_MIN);
-        mask |= (v ? 1u : 0u) << i;
+        any |= v;
         const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
         imin = better ? i : imin;
         ls = better ? l : ls;
     }
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
-    if (mask && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
+    if (any && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
         // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
         const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
         const float entry = fmaxf(root_entry, e);
@@ -561,12 +584,10 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
 #if RT_FASTDIV
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, false, true, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask,
-                                                           imin, ls);
+            found = stack_search<COUNT, false, true, true>(sc, k, r, ax, entry, root_exit, best, st, c, imin, ls);
         else
 #endif
-            found = stack_search<COUNT, false, false, true>(sc, k, r, ax, entry, root_exit, best, st, c, mask,
-                                                            imin, ls);
+            found = stack_search<COUNT, false, false, true>(sc, k, r, ax, entry, root_exit, best, st, c, imin, ls);
         if (found) return true;
     }
     if (sc.has_cube) {
@@ -1159,10 +1180,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
 #endif
 #if RT_LDS_SPHERES > 0
-    if (!GEN) {  // only the sphere-only kernel reads the LDS sphere table
-        k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-        for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
-    }
+    if (!GEN) fill_lds_spheres(sc, k);  // only the sphere-only kernel reads the LDS sphere tables
 #endif
 #if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
     if (!GEN || RT_LDS_NODES > 0) __syncthreads();
@@ -1273,10 +1291,7 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
 #endif
 #if RT_LDS_SPHERES > 0
-    if (!GEN) {  // only the sphere-only kernel reads the LDS sphere table
-        k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-        for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
-    }
+    if (!GEN) fill_lds_spheres(sc, k);  // only the sphere-only kernel reads the LDS sphere tables
 #endif
 #if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
     if (!GEN || RT_LDS_NODES > 0) __syncthreads();

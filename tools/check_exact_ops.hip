@@ -86,6 +86,31 @@ __global__ void k_norm(Stats* s, uint32_t rounds) {
     atomicAdd(&s->tested, n);
 }
 
+// sqrt_rn(x) = v_sqrt_f32 + the +-1 ulp FMA correction (trace.hip), without hipcc's denormal
+// scaling and class check: == sqrtf(x) for every x in [lo, +inf] (bit patterns), lo = 0 for
+// the full check; the per-range counts locate any failure
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    r = fmaf(-su, s, x) > 0.0f ? su : r;
+    return r;
+}
+__global__ void k_sqrt(Stats* s, uint32_t lo_bits) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long n = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (1ull << 31); i += stride) {
+        const uint32_t bits = (uint32_t)i;
+        const uint32_t ex = bits >> 23;
+        if (bits < lo_bits || bits > 0x7f800000u) continue;
+        (void)ex;
+        const float x = __uint_as_float(bits);
+        ++n;
+        if (__float_as_uint(sqrt_rn(x)) != __float_as_uint(sqrtf(x))) record(s, bits);
+    }
+    atomicAdd(&s->tested, n);
+}
+
 // theta = 2*pi*v for every v = j * 2^-24 in [0, 1): sincosf == (sinf, cosf)
 __global__ void k_sincos(Stats* s) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -110,13 +135,16 @@ static int report(const char* name, Stats* d) {
 
 int main() {
     Stats* d;
-    if (hipMalloc(&d, 4 * sizeof(Stats)) != hipSuccess) return 2;
-    (void)hipMemset(d, 0, 4 * sizeof(Stats));
+    if (hipMalloc(&d, 7 * sizeof(Stats)) != hipSuccess) return 2;
+    (void)hipMemset(d, 0, 7 * sizeof(Stats));
     // reciprocal over |b| in [2^-60, 2^60]: biased exponents 67..187
     hipLaunchKernelGGL(k_rcp, dim3(8192), dim3(256), 0, 0, d + 0, 67u, 187u);
     hipLaunchKernelGGL(k_div, dim3(8192), dim3(256), 0, 0, d + 1, 2048u);
     hipLaunchKernelGGL(k_norm, dim3(8192), dim3(256), 0, 0, d + 2, 1024u);
     hipLaunchKernelGGL(k_sincos, dim3((1u << 24) / 256), dim3(256), 0, 0, d + 3);
+    hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, d + 4, 47u << 23);  // [2^-80, inf]
+    hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, d + 5, 1u << 23);   // normals
+    hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, d + 6, 0u);         // everything >= 0
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     int bad = 0;
     std::printf("{");
@@ -127,6 +155,12 @@ int main() {
     bad |= report("normalize_quotients", d + 2);
     std::printf(", ");
     bad |= report("sincosf_vs_sinf_cosf", d + 3);
+    std::printf(", ");
+    bad |= report("sqrt_rn_2^-80_to_inf", d + 4);
+    std::printf(", ");
+    (void)report("sqrt_rn_normal_to_inf_info", d + 5);  // informational: fails below 2^-80
+    std::printf(", ");
+    (void)report("sqrt_rn_all_nonneg_info", d + 6);
     std::printf("}\n");
     (void)hipFree(d);
     return bad;
