@@ -31,6 +31,9 @@
 #ifndef RT_SMALL_SCENE
 #define RT_SMALL_SCENE 1    // exact brute-force-bounded traversal for <= 32 spheres (closest_small)
 #endif
+#ifndef RT_SMALL_SKIP
+#define RT_SMALL_SKIP 1     // closest_small: no traversal when the closest sphere provably is in the returning leaf
+#endif
 #ifndef RT_LEAF_PMIN
 #define RT_LEAF_PMIN 1      // closest_small: a leaf holding the closest sphere needs no re-test
 #endif
@@ -547,6 +550,39 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
     }
 }
 
+// Whether the closest sphere S (hit at L*, first minimum) is in the leaf the reference's
+// traversal returns from, decided without the traversal.  The visited leaves' intervals
+// [e_i, x_i] are contiguous and cover [root_entry, root_exit]; leaves with fl(x + EPS) < L*
+// cannot return (their best hit is >= L*), so the returning leaf is the first leaf k with
+// fl(x_k + EPS) >= L* if it holds S — whose candidate is then S at L* (leaf_closest's pmin
+// argument).  Such a leaf exists when fl(root_exit + EPS) >= L*; it has x_k > E (the descent
+// floor) and e_k <= L* (e_k = root_entry <= L*, or e_k = x_{k-1} < L*).  Below a branch (split
+// s on axis a, t_s = RN(RN(s - o_a) / d_a), monotone in s), leaves of the near child have
+// x <= t_s and leaves of the far child e >= t_s (kdtree.rs:79-87: intervals only shrink).  The
+// build puts S in the low child iff lo_a <= s and in the high child iff hi_a >= s
+// (kdtree.rs:119-127, lo/hi = fl(c -+ r), sphere.rs:106-114).  With d_a > 0: leaf k below the
+// low (near) child without S needs t(lo_a) >= t_s >= x_k > E; below the high (far) child,
+// t(hi_a) <= t_s <= e_k <= L*.  So t(near face) <= E and t(far face) > L* on every axis
+// (faces swap for d_a < 0) put S in leaf k whatever the tree.  t(face) is the traversal's
+// own arithmetic: the Markstein quotient with the ray's exact reciprocal, used only when
+// equal to the division (face - o in mk range); otherwise the traversal runs.
+__device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const RayAx& ax, float e, float ls) {
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float c = a == 0 ? s.x : (a == 1 ? s.y : s.z);
+        const float o = a == 0 ? r.o.x : (a == 1 ? r.o.y : r.o.z);
+        const float d = a == 0 ? ax.dx : (a == 1 ? ax.dy : ax.dz);
+        const float rc = a == 0 ? ax.rx : (a == 1 ? ax.ry : ax.rz);
+        const float nlo = (c - s.w) - o, nhi = (c + s.w) - o;
+        const float tlo = div_mk(nlo, d, rc), thi = div_mk(nhi, d, rc);
+        const float tn = d > 0.0f ? tlo : thi, tf = d > 0.0f ? thi : tlo;
+        ok &= mk_num(nlo) && mk_num(nhi);
+        ok &= (tn <= e) && (tf > ls);
+    }
+    return ok;
+}
+
 // KdTree::closest_ray_hit (kdtree.rs:58-64): root slab test, stack search, then the
 // unconditional renderables.  The Markstein division is used for the whole wave unless some
 // lane's origin (or the scene's splits) could underflow it.
@@ -579,6 +615,14 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
     if (any && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
         // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
         const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
+#if RT_SMALL_SKIP
+        if (!COUNT && root_entry <= ls && ls <= root_exit + EPS && in_return_leaf(fetch_sphere<false>(sc, k, imin), r, ax, e, ls)) {
+            best->ref = (K_SPHERE << REF_KIND_SHIFT) | imin;
+            best->l = ls;
+            best->bu = best->bv = 0.f;
+            return true;
+        }
+#endif
         const float entry = fmaxf(root_entry, e);
         bool found;
 #if RT_FASTDIV

@@ -191,3 +191,82 @@ def test_queue_schedule_bit_invariant(gpu_available, monkeypatch, scene_name, sp
         g2 = cq.render(tiles, spp, 4)
     assert np.array_equal(g, ref)
     assert np.array_equal(g2, ref2)
+
+
+def _adversarial_spheres(seed: int) -> dict:
+    """<= 32 spheres built to make the closest-hit decision hard: duplicates (exact ties),
+    concentric shells 1e-4 apart, tangent pairs, tiny spheres, deep overlaps and r = 500 walls
+    (hits near their poles).  Each sphere emits a distinct colour, so a first-hit image says
+    which sphere every camera ray returned."""
+    rng = np.random.default_rng(seed)
+    sph = []
+    for c, r in (((515.0, 0.0, -10.0), 500.0), ((-515.0, 0.0, -10.0), 500.0),
+                 ((0.0, -510.0, -10.0), 500.0), ((0.0, 0.0, -530.0), 500.0)):
+        sph.append((c, r))
+    while len(sph) < 30:
+        kind = rng.integers(0, 5)
+        c = rng.uniform(-6.0, 6.0, 3).astype(np.float32)
+        r = np.float32(rng.uniform(0.2, 3.0))
+        if kind == 0:                        # exact duplicate of an earlier sphere
+            sph.append(sph[rng.integers(4, len(sph))] if len(sph) > 4 else (tuple(c), r))
+        elif kind == 1:                      # concentric shells
+            sph.append((tuple(c), r))
+            sph.append((tuple(c), np.float32(r + 1e-4)))
+        elif kind == 2:                      # tangent pair
+            u = rng.normal(size=3)
+            u /= np.linalg.norm(u)
+            r2 = np.float32(rng.uniform(0.2, 2.0))
+            sph.append((tuple(c), r))
+            sph.append((tuple(np.float32(c + (r + r2) * u)), r2))
+        elif kind == 3:                      # tiny sphere
+            sph.append((tuple(c), np.float32(rng.uniform(1e-3, 2e-2))))
+        else:
+            sph.append((tuple(c), r))
+    sph = sph[:30]
+    members = []
+    for i, (c, r) in enumerate(sph):
+        em = [(i + 1) / 32.0, ((i * 7) % 31 + 1) / 32.0, ((i * 13) % 29 + 1) / 32.0]
+        members.append({"!Sphere": {"c": [float(x) for x in c], "r": float(r),
+                                    "coloring": {"!Solid": [0.5, 0.5, 0.5]},
+                                    "mat": {"divert_ray": "Diff", "emissive": em}}})
+    # camera: inside the cluster; on a sphere's surface looking out; grazing the floor wall
+    # (hits near its pole); inside the floor wall sphere
+    i = int(rng.integers(4, len(sph)))
+    u = rng.normal(size=3)
+    u /= np.linalg.norm(u)
+    d = rng.normal(size=3)
+    d[1] *= 0.3
+    kind = seed % 4
+    if kind == 0:
+        o = rng.uniform(-4.0, 4.0, 3)
+    elif kind == 1:
+        o = np.float32(np.array(sph[i][0]) + sph[i][1] * u)
+        d = u + 0.3 * rng.normal(size=3)
+    elif kind == 2:
+        o = np.array([rng.uniform(-3, 3), -9.9, rng.uniform(-8, 2)])
+        d[1] = -abs(d[1]) * 0.2
+    else:
+        o = np.array([0.0, -10.5, -10.0])
+    d = 5.0 * d / np.linalg.norm(d)
+    return {"cam": {"d": [float(x) for x in d], "o": [float(x) for x in o], "screen_height": 5.0,
+                    "screen_width": 10.0, "up": [0, 1, 0], "view_eulers": [0, 0, 0]},
+            "render_info": {"gpu_render_batch": 1, "height": 96, "width": 160, "kd_tree_depth": 17,
+                            "rad_info": {"debug_single_ray": True, "dir_light_samp": False,
+                                         "russ_roull_info": {"assured_depth": 5, "max_thres": 0.5}},
+                            "samps_per_pix": 1, "use_gpu": True},
+            "scene_members": members}
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_small_scene_closest_sphere_bit_exact(gpu_available, oracle, seed):
+    """closest_small's exact shortcuts (descent floor, pmin leaf, no traversal when the closest
+    sphere is provably in the returning leaf) against the oracle's full KD traversal, first hit
+    only, on adversarial sphere sets: the returned sphere must match for every ray."""
+    from rt_amd import render, scheme
+
+    sc = scheme.load(_adversarial_spheres(seed))
+    tiles = [(0, 0, 160, 96)]
+    with render.Context(sc) as c:
+        g = c.render(tiles, 0, 3)
+    o = oracle.render(sc, tiles, 0, 3)
+    assert np.array_equal(g, o), parity.stats(g, o)
