@@ -31,6 +31,9 @@
 #ifndef RT_SMALL_SCENE
 #define RT_SMALL_SCENE 1    // exact brute-force-bounded traversal for <= 32 spheres (closest_small)
 #endif
+#ifndef RT_DISC_SKIP
+#define RT_DISC_SKIP 1      // closest_small: skip a sphere's roots when no lane's discriminant is positive
+#endif
 #ifndef RT_SMALL_SKIP
 #define RT_SMALL_SKIP 1     // closest_small: no traversal when the closest sphere provably is in the returning leaf
 #endif
@@ -197,6 +200,7 @@ __shared__ uint2 g_lds_nodes[RT_LDS_NODES];
 #endif
 #if RT_LDS_SPHERES > 0
 __shared__ float4 g_lds_sph[RT_LDS_SPHERES];
+__shared__ float4 g_lds_csq[RT_LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
 #endif
 struct Cache {
     uint32_t n_nodes;  // nodes [0, n_nodes) are in g_lds_nodes
@@ -223,27 +227,40 @@ __device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, const Cache& 
 #if RT_LDS_SPHERES > 0
 __device__ __forceinline__ void fill_lds_spheres(const DevScene& sc, Cache& k) {
     k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) g_lds_sph[i] = sc.sph[i];
+    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) {
+        const float4 v = sc.sph[i];
+        g_lds_sph[i] = v;
+        g_lds_csq[i] = make_float4(v.x, v.y, v.z, v.w * v.w);
+    }
 }
 #endif
 
 // ---------------------------------------------------------------- primitives
-// Sphere::intersect (sphere.rs:83-105)
-// Branch-free: sqrt of max(thing2, 0) equals sqrt(thing2) whenever the hit is taken.  With p0
-// and p1 both true neither root is NaN or zero, so a compare-select is fminf (without its NaN
-// canonicalisation).
-__device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
+// Sphere::intersect (sphere.rs:83-105) in two steps: the discriminant (sphere_disc, with
+// rr = fl(r * r)), then the roots (sphere_roots), so the brute-force loop can skip the second
+// step for a sphere no lane of the wave meets.  Branch-free: sqrt of max(thing2, 0) equals
+// sqrt(thing2) whenever the hit is taken.  thing >= 0 gives l1 = RN(offset - thing) <=
+// l0 = RN(offset + thing), so p1 implies p0, filter(>0).reduce(min) is `p1 ? l1 : l0`, and a
+// hit is disc && p0 (a miss's *l is never used).
+struct SphDisc {
+    float dir, thing2;
+};
+__device__ __forceinline__ SphDisc sphere_disc(float4 s, float rr, const Ray& r) {
     const V3 oc = r.o - xyz(s);
     const float dir = dot(r.d, oc);
-    const float consts = dot(oc, oc) - s.w * s.w;
-    const float thing2 = dir * dir - consts;
-    const bool disc = thing2 > 0.0f;
-    const float offset = -dir;
-    const float thing = sqrt_nonneg(fmaxf(thing2, 0.0f));
+    const float consts = dot(oc, oc) - rr;
+    return SphDisc{dir, dir * dir - consts};
+}
+__device__ __forceinline__ bool sphere_roots(SphDisc q, float* l) {
+    const bool disc = q.thing2 > 0.0f;
+    const float offset = -q.dir;
+    const float thing = sqrt_nonneg(fmaxf(q.thing2, 0.0f));
     const float l0 = offset + thing, l1 = offset - thing;
-    const bool p0 = l0 > 0.0f, p1 = l1 > 0.0f;
-    *l = p0 ? (p1 ? (l1 < l0 ? l1 : l0) : l0) : l1;  // filter(>0).reduce(min), sphere.rs:95
-    return disc && (p0 || p1);
+    *l = l1 > 0.0f ? l1 : l0;  // sphere.rs:95
+    return disc && l0 > 0.0f;
+}
+__device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
+    return sphere_roots(sphere_disc(s, s.w * s.w, r), l);
 }
 
 // Triangle::intersect, Möller–Trumbore (triangle/generic.rs:102-137)
@@ -592,8 +609,9 @@ __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const Ray
 // with fl(exit + EPS) < L* can never return.  Descending from entry E, where
 // fl(E + EPS) < L* holds for every value <= E, skips exactly such leaves (a near child whose
 // interval ends at or before E is not entered) and leaves every other leaf's interval, order
-// and exit untouched — so the returned sphere and distance are the reference's.  The
-// instrumented (COUNT) kernel keeps the plain traversal: its counters are the reference's work.
+// and exit untouched — so the returned sphere and distance are the reference's.  Most rays
+// need no descent at all (in_return_leaf).  The instrumented kernel counts the reference's work with the plain traversal and the device's
+// work (count_device) through this function.
 template <bool COUNT>
 __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                               uint32_t* st, Ctr<COUNT>& c) {
@@ -603,8 +621,11 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
     if (COUNT) c.sph += sc.n_spheres;
 #pragma unroll RT_SPH_UNROLL
     for (uint32_t i = 0; i < sc.n_spheres; ++i) {
+        const float4 sq = g_lds_csq[i];
+        const SphDisc q = sphere_disc(sq, sq.w, r);
+        if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) continue;  // v false on every lane
         float l;
-        const bool v = sphere_hit(fetch_sphere<false>(sc, k, i), r, &l) & !(l < HIT_MIN);
+        const bool v = sphere_roots(q, &l) & !(l < HIT_MIN);
         any |= v;
         const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
         imin = better ? i : imin;
@@ -616,7 +637,8 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
         // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
         const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
 #if RT_SMALL_SKIP
-        if (!COUNT && root_entry <= ls && ls <= root_exit + EPS && in_return_leaf(fetch_sphere<false>(sc, k, imin), r, ax, e, ls)) {
+        // (COUNT here means the device-work count: closest_small never runs for the reference's)
+        if (root_entry <= ls && ls <= root_exit + EPS && in_return_leaf(fetch_sphere<false>(sc, k, imin), r, ax, e, ls)) {
             best->ref = (K_SPHERE << REF_KIND_SHIFT) | imin;
             best->l = ls;
             best->bu = best->bv = 0.f;
