@@ -144,9 +144,9 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     const float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
     return fmaf(-su, s, x) > 0.0f ? su : r;
 }
-// sqrtf(x) for x = fmaxf(y, 0) (never NaN, never below -0).  bits - 1 wraps for +0 and is
-// >= 0x7fffffff for -0, so one compare sends exactly (0, 2^-80) to sqrtf — a divergent branch
-// no lane normally takes.
+// sqrtf(x) for x >= -0 (an fmaxf(y, 0), a dot(a, a), a uniform draw).  bits - 1 wraps for +0
+// and is >= 0x7fffffff for -0, so one compare sends exactly (0, 2^-80) to sqrtf — a divergent
+// branch no lane normally takes.  (A NaN x gives a NaN either way.)
 __device__ __forceinline__ float sqrt_nonneg(float x) {
     if (!RT_EXACT_FAST) return sqrtf(x);
     float s = sqrt_rn(x);
@@ -154,7 +154,7 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
     return s;
 }
 __device__ __forceinline__ V3 normalize(V3 a) {
-    float n = sqrtf(dot(a, a));
+    float n = sqrt_nonneg(dot(a, a));
     return div3(a, n);
 }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
@@ -905,7 +905,7 @@ __device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
     V3 yd = normalize(cross(n, xd));
     float u = draw(rng);
     float v = draw(rng);
-    float r = sqrtf(u);
+    float r = sqrt_nonneg(u);
     float thet = 2.0f * PI * v;
     float sn, cs;
 #if RT_EXACT_FAST
@@ -916,7 +916,7 @@ __device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
 #endif
     float x = r * cs;
     float y = r * sn;
-    return normalize((xd * x + yd * y) + n * sqrtf(fmaxf(1.0f - u, 0.0f)));
+    return normalize((xd * x + yd * y) + n * sqrt_nonneg(fmaxf(1.0f - u, 0.0f)));
 }
 __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, float* p,
                                           uint32_t* rng) {  // :29-59
@@ -929,7 +929,7 @@ __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, f
     float c22 = 1.0f - n_over * n_over * (1.0f - c1 * c1);
     V3 refl = spec_dir(d, norm_refr);
     if (c22 < 0.0f) { *p = 1.0f; return refl; }
-    V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrtf(c22));
+    V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrt_nonneg(c22));  // c22 >= 0 here
     float q = (n1 - n2) / (n1 + n2);
     float r0 = q * q;
     float c = 1.0f - (into ? c1 : dot(trns, n));
@@ -987,7 +987,7 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint
         float a = sc.lens_r;
         float u = draw(rng);
         float v = draw(rng);
-        float r = sqrtf(u);
+        float r = sqrt_nonneg(u);
         float thet = 2.0f * PI * v;
         float sn, cs;
         sincosf(thet, &sn, &cs);
