@@ -12,14 +12,15 @@
 // the branch that pushed it; t and the exit distance are recomputed on pop.
 //
 // Float order matches the oracle operation for operation (compiled with -ffp-contract=off,
-// correctly rounded div/sqrt); the only intended differences are the accumulation order of
-// the bounce estimator (forward L += T*e instead of the reference's recursion) and ocml's
-// sinf/cosf/powf against glibc's — DESIGN.md §Numerics.
+// correctly rounded div/sqrt, and glibc's sinf/cosf/powf restated in include/rt_libm.h); the
+// only intended difference is the accumulation order of the bounce estimator (forward
+// L += T*e instead of the reference's recursion) — DESIGN.md §Numerics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../../include/rt_abi.h"
 #include "../../../include/rt_rng.h"
+#include "../../../include/rt_libm.h"
 #include "device_scene.h"
 
 #ifndef RT_LDS_NODES
@@ -908,12 +909,7 @@ __device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
     float r = sqrt_nonneg(u);
     float thet = 2.0f * PI * v;
     float sn, cs;
-#if RT_EXACT_FAST
-    sincosf(thet, &sn, &cs);  // == (sinf, cosf) bit for bit (tools/check_exact_ops.hip)
-#else
-    sn = sinf(thet);
-    cs = cosf(thet);
-#endif
+    (void)rt_sincosf(thet, &sn, &cs);  // glibc's sinf, cosf (rt_libm.h); thet in [0, 2 pi)
     float x = r * cs;
     float y = r * sn;
     return normalize((xd * x + yd * y) + n * sqrt_nonneg(fmaxf(1.0f - u, 0.0f)));
@@ -933,7 +929,7 @@ __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, f
     float q = (n1 - n2) / (n1 + n2);
     float r0 = q * q;
     float c = 1.0f - (into ? c1 : dot(trns, n));
-    float re = r0 + (1.0f + r0) * powf(c, 5.0f);
+    float re = r0 + (1.0f + r0) * rt_powf5(c);  // glibc's powf(c, 5)
     float u = draw(rng);
     if (u < re) { *p = re; return refl; }
     *p = 1.0f - re;
@@ -990,7 +986,7 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint
         float r = sqrt_nonneg(u);
         float thet = 2.0f * PI * v;
         float sn, cs;
-        sincosf(thet, &sn, &cs);
+        (void)rt_sincosf(thet, &sn, &cs);  // thet in [0, 2 pi)
         float lx = (r - 0.5f) * 2.0f * a * cs;
         float ly = (r - 0.5f) * 2.0f * a * sn;
         V3 off = right * lx + up * ly;
@@ -1111,7 +1107,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
         rough = mr.y * pr.rough;
     }
     const float r0 = 0.04f + (1.0f - 0.04f) * metal;
-    const float reflectance = r0 + (1.0f - r0) * 1.0f * (1.0f - powf(fabsf(dot(p.ray.d, n)), 5.0f));
+    const float reflectance = r0 + (1.0f - r0) * 1.0f * (1.0f - rt_powf5(fabsf(dot(p.ray.d, n))));
     const bool should_diff = draw(&p.rng) < 1.0f - reflectance;  // DynDiffSpec::should_diff
     const V3 pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
     if (sc.debug_single_ray) return true;

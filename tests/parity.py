@@ -1,9 +1,10 @@
 """Per-pixel comparison used by the -m gpu parity tests (tolerances stated in DESIGN.md §Parity).
 
 Gate: per-pixel L-inf over RGB <= REL_TOL * max(1, |ref|) on at least
-MIN_FRAC of the pixels.  Pixels outside it come from path-divergent branch flips (a ULP
-difference in ocml vs glibc sinf/cosf/powf moves a ray across a silhouette): each is bounded
-by the scene's largest path contribution / spp and they are counted, not hidden.
+MIN_FRAC of the pixels.  Against the forward oracle the device is bit-identical (glibc's
+transcendentals restated in include/rt_libm.h); against the recursive oracle only the
+accumulation order differs.  Any pixel outside the gate would be a path-divergent branch flip:
+they are counted, not hidden.
 """
 import numpy as np
 
