@@ -59,6 +59,27 @@ def committed_traffic(scene, samples_per_launch):
     return best
 
 
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: SIMD-32, a wave's instruction issues over 2 cycles) at 2.4 GHz
+VALU_PEAK_WINST_S = 256 * 4 * 2.4e9 / 2
+
+
+def committed_valu(scene, samples_per_launch):
+    """VALU wave-instructions per launch (and lane utilisation) from the committed rocprofv3 SQ
+    passes of the same workload (profiles/*_valu.json, written by tools/prof_summary.py)."""
+    import glob
+
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("scene") == scene and d.get("samples_per_launch") == samples_per_launch:
+            best = (d, os.path.relpath(p, ROOT))
+    return best
+
+
 def cpu_baseline(loaded, target_s=10.0, threads=None):
     """The oracle (C++ restatement of render_to_target_cpu) on this host's cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -87,6 +108,18 @@ def cpu_baseline(loaded, target_s=10.0, threads=None):
             "kind": "port",
             "sample": f"full {w}x{h} frame, {spp} spp in one call (KD build included, as per frame in "
                       f"the reference), oracle/oracle.cpp recursive radiance, {threads} threads, {dt:.1f} s"}
+
+
+def valu_roofline(scene, samples_per_launch, kernel_ms):
+    """The bound the kernel actually runs against: VALU instruction issue."""
+    c = committed_valu(scene, samples_per_launch)
+    if not c:
+        return None
+    d, src = c
+    rate = d["valu_insts_per_launch"] / (kernel_ms * 1e-3)
+    return {"insts_per_launch": d["valu_insts_per_launch"], "achieved_winst_per_s": round(rate / 1e9, 1),
+            "peak_winst_per_s": round(VALU_PEAK_WINST_S / 1e9, 1), "unit": "G wave-instructions/s",
+            "frac": round(rate / VALU_PEAK_WINST_S, 4), "lane_util": d.get("valu_lane_util"), "source": src}
 
 
 def main():
@@ -227,6 +260,7 @@ def main():
                            "device_frac": round(dev_bps * per_launch / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "device_counts_per_sample": {k: round(v / dev_counts["samples"], 3)
                                                         for k, v in dev_counts.items() if k != "samples"},
+                           "valu": valu_roofline(args.scene, round(per_launch), avg_ms),
                            "note": "achieved/frac price the REFERENCE algorithm's bytes per sample (SURVEY.md "
                                    "§8d, counted by rt_count_work); the device skips provably non-returning "
                                    "KD leaves (closest_small), so frac can exceed 1; device_frac prices the "

@@ -42,6 +42,7 @@ def main(tag):
             if l.startswith("{"):
                 d = json.loads(l)
                 lines += ["## bench.py line (under the profiler)", "", "```", l.strip(), "```", ""]
+    valu = {}
     for part, title in (("fetch", "HBM read bytes (FETCH_SIZE, own pass)"), ("sq", "SQ counters (own pass)"),
                         ("sq2", "SQ lane utilisation (own pass)")):
         p = os.path.join(src, part, "run_counter_collection.csv")
@@ -72,6 +73,10 @@ def main(tag):
                        "note": "rocprofv3 --pmc FETCH_SIZE, own pass, last trace dispatch, x2 per "
                                "MI355X_MICROARCH.md HBM section"},
                       open(os.path.join(dst, f"{tag}_fetch.json"), "w"), indent=1)
+        if "SQ_INSTS_VALU" in d:
+            valu["valu_insts_per_launch"] = d["SQ_INSTS_VALU"]
+        if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
+            valu["valu_lane_util"] = round(d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_ACTIVE_INST_VALU"]), 4)
         if "SQ_WAVE_CYCLES" in d:
             wc = d["SQ_WAVE_CYCLES"]
             lines.append(f"\nLast dispatch: wait-any {d.get('SQ_WAIT_ANY', 0) / wc:.1%}, issuing {d.get('SQ_ACTIVE_INST_ANY', 0) / wc:.1%}, "
@@ -80,6 +85,18 @@ def main(tag):
             lines.append(f"\nLast dispatch: VALU lane utilisation = THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU) = "
                          f"{d['SQ_THREAD_CYCLES_VALU'] / (64 * d['SQ_ACTIVE_INST_VALU']):.1%}.")
         lines.append("")
+    if "valu_insts_per_launch" in valu:
+        bl = os.path.join(src, "bench_sq.log")
+        cfg = {}
+        if os.path.exists(bl):
+            for l in open(bl):
+                if l.startswith("{"):
+                    cfg = json.loads(l)
+        valu.update({"scene": cfg.get("metric", "").split(" on ")[-1].replace(".yml", "") if cfg else None,
+                     "samples_per_launch": cfg.get("launch", {}).get("samples_per_launch", 0),
+                     "note": "rocprofv3 --pmc SQ_INSTS_VALU (wave-level VALU instructions, all XCDs) and "
+                             "THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU), own passes, last trace dispatch"})
+        json.dump(valu, open(os.path.join(dst, f"{tag}_valu.json"), "w"), indent=1)
     out = os.path.join(dst, f"{tag}_summary.md")
     open(out, "w").write("\n".join(lines) + "\n")
     print(open(out).read())
