@@ -5,7 +5,7 @@ One step = one launch of the megakernel over this rank's pixels for `--spp-per-s
 (the reference's gpu_render_batch, walled.yml: 1000), plus — for N > 1 — the frame-end RCCL
 gather of every rank's tile radiance to rank 0.  Inputs (scene, KD tree) are resident in HBM
 before the timed region.  N GPUs: one process per GPU (torch.distributed.run), image rows
-sharded as 4-row stripes dealt round-robin.  Weak scaling: at N GPUs a step renders N x
+sharded as 1-row stripes dealt round-robin.  Weak scaling: at N GPUs a step renders N x
 spp-per-step samples for every pixel, so each rank keeps the work of the 1-GPU step
 (W*H/N pixels x N*spp samples) and the image stays bit-identical to the 1-GPU one (the RNG and
 the running mean are keyed on the global pixel and absolute sample index).

@@ -121,6 +121,7 @@ struct LaunchArgs {
     DevScene sc;
     const DevTile* tiles;
     uint32_t n_tiles;
+    const uint32_t* pix_xy; // launch pixel o -> (y << 16) | x; nullptr for frames over 65535 wide/high
     uint32_t n_blocks;
     uint64_t sample_begin;
     uint32_t sample_count;

@@ -1316,6 +1316,20 @@ __device__ __forceinline__ uint32_t tile_of(const LaunchArgs& a, uint32_t o) {
     }
     return lo;
 }
+// Frame coordinates of launch pixel o: one coalesced load from the host-built table, or (frames
+// over 65535 pixels wide or high) a binary search over the tiles.
+__device__ __forceinline__ void launch_pixel(const LaunchArgs& a, uint32_t o, int* x, int* y) {
+    if (a.pix_xy) {
+        const uint32_t v = a.pix_xy[o];
+        *x = (int)(v & 0xffffu);
+        *y = (int)(v >> 16);
+        return;
+    }
+    const DevTile tl = a.tiles[tile_of(a, o)];
+    const uint32_t lo = o - tl.out_off;
+    *x = (int)(tl.x0 + lo % tl.w);
+    *y = (int)(tl.y0 + lo / tl.w);
+}
 
 // Queue schedule: the grid is sized to the resident lanes, and every lane keeps tracing
 // (pixel, sample) items until the launch's items are exhausted, so a wave is never held back
@@ -1385,9 +1399,8 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
                 const uint32_t item = r < left ? pool + r : base + (r - left);
                 if (item < a.n_items) {
                     const uint32_t j = item / a.n_pix, o = item - j * a.n_pix;
-                    const DevTile tl = a.tiles[tile_of(a, o)];
-                    const uint32_t lo = o - tl.out_off;
-                    const int x = (int)(tl.x0 + lo % tl.w), y = (int)(tl.y0 + lo / tl.w);
+                    int x, y;
+                    launch_pixel(a, o, &x, &y);
                     start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
                     slot = item;
                     have = true;
@@ -1498,9 +1511,8 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
                 const uint32_t item = rk < left ? pool + rk : base + (rk - left);
                 if (item < a.n_items) {
                     const uint32_t j = item / a.n_pix, o = item - j * a.n_pix;
-                    const DevTile tl = a.tiles[tile_of(a, o)];
-                    const uint32_t lo = o - tl.out_off;
-                    const int x = (int)(tl.x0 + lo % tl.w), y = (int)(tl.y0 + lo / tl.w);
+                    int x, y;
+                    launch_pixel(a, o, &x, &y);
                     start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
                     slot = item;
                     have = true;
@@ -1600,18 +1612,36 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
 __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
     const uint32_t o = blockIdx.x * 256 + threadIdx.x;
     if (o >= a.n_pix) return;
-    uint32_t t = 0;
-    while (t + 1 < a.n_tiles && a.tiles[t + 1].out_off <= o) ++t;
-    const DevTile tl = a.tiles[t];
-    const uint32_t lo = o - tl.out_off;
-    const uint32_t pix = (tl.y0 + lo / tl.w) * a.sc.width + tl.x0 + lo % tl.w;
+    int x, y;
+    launch_pixel(a, o, &x, &y);
+    const uint32_t pix = (uint32_t)y * a.sc.width + (uint32_t)x;
     V3 acc = mk(0.f, 0.f, 0.f);
     if (a.sample_begin > 0) acc = xyz(a.accum[pix]);
-    for (uint32_t j = 0; j < a.sample_count; ++j) {
+    // (r + acc n) / (n + 1) per channel, in sample order; div3 is the division bit for bit
+    // (exact reciprocal + Markstein quotients under their range guard).  The samples' loads are
+    // issued FOLD_U at a time ahead of the sequential fold: with few launch pixels (a rank's
+    // share at N = 8: 90K threads) one load in flight per thread left the fold latency-bound.
+    constexpr uint32_t FOLD_U = 8;
+    uint32_t j = 0;
+    for (; j + FOLD_U <= a.sample_count; j += FOLD_U) {
+        float v[3 * FOLD_U];
+#pragma unroll
+        for (uint32_t u = 0; u < FOLD_U; ++u) {
+            const float* r = a.radiance + 3 * ((size_t)(j + u) * a.n_pix + o);
+            v[3 * u] = r[0];
+            v[3 * u + 1] = r[1];
+            v[3 * u + 2] = r[2];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < FOLD_U; ++u) {
+            const float n = (float)(a.sample_begin + j + u);
+            acc = div3(mk(v[3 * u] + (acc.x * n), v[3 * u + 1] + (acc.y * n), v[3 * u + 2] + (acc.z * n)), n + 1.0f);
+        }
+    }
+    for (; j < a.sample_count; ++j) {
         const float* r = a.radiance + 3 * ((size_t)j * a.n_pix + o);
         const float n = (float)(a.sample_begin + j);
-        acc = mk((r[0] + (acc.x * n)) / (n + 1.0f), (r[1] + (acc.y * n)) / (n + 1.0f),
-                 (r[2] + (acc.z * n)) / (n + 1.0f));
+        acc = div3(mk(r[0] + (acc.x * n), r[1] + (acc.y * n), r[2] + (acc.z * n)), n + 1.0f);
     }
     const float4 ov = make_float4(acc.x, acc.y, acc.z, 1.0f);
     a.accum[pix] = ov;

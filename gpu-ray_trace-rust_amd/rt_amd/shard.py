@@ -7,7 +7,7 @@ depend on which rank renders it (RNG and running mean are keyed on the global pi
 absolute sample), so the assembled frame equals the 1-GPU frame bit for bit."""
 from __future__ import annotations
 
-STRIPE = 4  # rows
+STRIPE = 1  # rows: 600- and 4096-row frames split evenly over 2, 4 and 8 ranks
 
 
 def rank_tiles(width: int, height: int, rank: int, world: int, stripe: int = STRIPE):
