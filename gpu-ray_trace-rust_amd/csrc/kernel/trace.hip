@@ -59,6 +59,9 @@
 #ifndef RT_DPP_SCAN
 #define RT_DPP_SCAN 1       // wave prefix sums by DPP row shifts / broadcasts (else ds_bpermute)
 #endif
+#ifndef RT_TIMING
+#define RT_TIMING 0         // diagnostic build: wave-clock breakdown (rt_debug_timing), never the product
+#endif
 #ifndef RT_OWNER_SCAN
 #define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
 #endif
@@ -708,6 +711,14 @@ __shared__ unsigned long long g_coop_key[BLOCK];
 __shared__ uint32_t g_coop_slot[BLOCK];
 #endif
 
+#if RT_TIMING
+// Diagnostic build only (-DRT_TIMING=1): wave-clock breakdown of the general queue kernel.
+// [0] descent + pop cycles, [1] cooperative pass cycles, [2] traversal rounds, [3] passes,
+// [4] queue-kernel cycles, [5] closest_coop calls (all summed over waves).
+__device__ unsigned long long g_rt_timing[8];
+#define RT_CLOCK() __builtin_amdgcn_s_memtime()
+#endif
+
 // Inclusive prefix maximum over the 64 lanes (the DPP pattern of wave_incl_scan with max).
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
@@ -811,7 +822,14 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
     int sp = 0;
     bool done = !active, found = false;
     const uint32_t lane = __lane_id();
+#if RT_TIMING
+    unsigned long long t_desc = 0, t_pass = 0, rounds = 0, passes = 0;
+#endif
     while (__ballot(!done) != 0) {
+#if RT_TIMING
+        const unsigned long long T0 = RT_CLOCK();
+        ++rounds;
+#endif
         uint32_t off = 0, cnt = 0;
         if (!done) {
             uint2 nd = fetch_node(sc, k, node);
@@ -832,7 +850,16 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
             off = nd.y >> 2;
             cnt = nd.x;
         }
+#if RT_TIMING
+        passes += (__shfl(wave_incl_scan(cnt, lane), 63) + 63) / 64;
+        const unsigned long long T1 = RT_CLOCK();
+#endif
         const unsigned long long key = coop_leaf(sc, r, off, cnt, lane);
+#if RT_TIMING
+        const unsigned long long T2 = RT_CLOCK();
+        t_pass += T2 - T1;
+        t_desc += T1 - T0;
+#endif
         if (!done) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
@@ -867,7 +894,19 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
                 }
             }
         }
+#if RT_TIMING
+        t_desc += RT_CLOCK() - T2;
+#endif
     }
+#if RT_TIMING
+    if (lane == 0) {
+        atomicAdd(&g_rt_timing[0], t_desc);
+        atomicAdd(&g_rt_timing[1], t_pass);
+        atomicAdd(&g_rt_timing[2], rounds);
+        atomicAdd(&g_rt_timing[3], passes);
+        atomicAdd(&g_rt_timing[5], 1ull);
+    }
+#endif
     return found;
 }
 
@@ -1381,6 +1420,9 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
+#if RT_TIMING
+    const unsigned long long T_start = RT_CLOCK();
+#endif
     for (;;) {
         const uint64_t need = __ballot(!have && !done);
         if (need) {
@@ -1416,7 +1458,12 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
                 pool += n;
             }
         }
-        if (__ballot(have) == 0) break;
+        if (__ballot(have) == 0) {
+#if RT_TIMING
+            if (GEN && lane == 0) atomicAdd(&g_rt_timing[4], RT_CLOCK() - T_start);
+#endif
+            break;
+        }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const bool fin = (GEN && RT_COOP) ? segment<false, GEN, DLS, GEN && RT_COOP>(sc, k, p, st, c, have) && have
                                           : have && segment<false, GEN, DLS>(sc, k, p, st, c);
@@ -1647,6 +1694,17 @@ __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
     a.accum[pix] = ov;
     if (a.out) a.out[o] = ov;
 }
+
+#if RT_TIMING
+extern "C" int rt_debug_timing(unsigned long long out[8], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_timing), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt_timing), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_fold(const LaunchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(fold_kernel, dim3((a.n_pix + 255) / 256), dim3(256), 0, s, a);
