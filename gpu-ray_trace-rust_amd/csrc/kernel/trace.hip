@@ -65,6 +65,9 @@
 #ifndef RT_OWNER_SCAN
 #define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
 #endif
+#ifndef RT_SPH_PREFETCH
+#define RT_SPH_PREFETCH 0   // closest_small: next sphere's LDS record read ahead of the current test
+#endif
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
@@ -242,8 +245,8 @@ __device__ __forceinline__ void fill_lds_spheres(const DevScene& sc, Cache& k) {
 // ---------------------------------------------------------------- primitives
 // Sphere::intersect (sphere.rs:83-105) in two steps: the discriminant (sphere_disc, with
 // rr = fl(r * r)), then the roots (sphere_roots), so the brute-force loop can skip the second
-// step for a sphere no lane of the wave meets.  Branch-free: sqrt of max(thing2, 0) equals
-// sqrt(thing2) whenever the hit is taken.  thing >= 0 gives l1 = RN(offset - thing) <=
+// step for a sphere no lane of the wave meets.  Branch-free: the root is taken of thing2 as is,
+// and used only when thing2 > 0.  thing >= 0 gives l1 = RN(offset - thing) <=
 // l0 = RN(offset + thing), so p1 implies p0, filter(>0).reduce(min) is `p1 ? l1 : l0`, and a
 // hit is disc && p0 (a miss's *l is never used).
 struct SphDisc {
@@ -258,7 +261,8 @@ __device__ __forceinline__ SphDisc sphere_disc(float4 s, float rr, const Ray& r)
 __device__ __forceinline__ bool sphere_roots(SphDisc q, float* l) {
     const bool disc = q.thing2 > 0.0f;
     const float offset = -q.dir;
-    const float thing = sqrt_nonneg(fmaxf(q.thing2, 0.0f));
+    // thing2 <= 0 (or NaN) gives a NaN or 0 here, but then disc is false and *l is never used
+    const float thing = sqrt_nonneg(q.thing2);
     const float l0 = offset + thing, l1 = offset - thing;
     *l = l1 > 0.0f ? l1 : l0;  // sphere.rs:95
     return disc && l0 > 0.0f;
@@ -623,9 +627,17 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
     bool any = false;
     float ls = __builtin_inff();
     if (COUNT) c.sph += sc.n_spheres;
+#if RT_SPH_PREFETCH
+    float4 sq_next = g_lds_csq[0];
+#endif
 #pragma unroll RT_SPH_UNROLL
     for (uint32_t i = 0; i < sc.n_spheres; ++i) {
+#if RT_SPH_PREFETCH
+        const float4 sq = sq_next;
+        sq_next = g_lds_csq[i + 1];  // the table has RT_LDS_SPHERES > 32 entries
+#else
         const float4 sq = g_lds_csq[i];
+#endif
         const SphDisc q = sphere_disc(sq, sq.w, r);
         if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) continue;  // v false on every lane
         float l;
