@@ -160,9 +160,25 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
     if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
     return s;
 }
+#ifndef RT_NORM_GUARD
+#define RT_NORM_GUARD 1     // normalize: the Markstein range guard by float compares (see below)
+#endif
+// nalgebra normalize: a / |a| per component.  div3's guard, specialised: |a_i| < 2^60 follows
+// from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs
+// "zero or |a_i| >= 2^-60" — one compare with a free abs modifier and one equality.  A NaN
+// numerator makes |a| NaN, which fails mk_range.
+__device__ __forceinline__ bool tiny_ok(float x) { return !(fabsf(x) < 0x1p-60f) || x == 0.0f; }
 __device__ __forceinline__ V3 normalize(V3 a) {
     float n = sqrt_nonneg(dot(a, a));
+#if RT_NORM_GUARD
+    if (!RT_EXACT_FAST) return a / n;
+    const float r = rcp_exact(n);
+    V3 q = mk(div_mk(a.x, n, r), div_mk(a.y, n, r), div_mk(a.z, n, r));
+    if (__builtin_expect(!(mk_range(n) && tiny_ok(a.x) && tiny_ok(a.y) && tiny_ok(a.z)), 0)) q = a / n;
+    return q;
+#else
     return div3(a, n);
+#endif
 }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -724,9 +740,10 @@ __shared__ uint32_t g_coop_slot[BLOCK];
 #endif
 
 #if RT_TIMING
-// Diagnostic build only (-DRT_TIMING=1): wave-clock breakdown of the general queue kernel.
-// [0] descent + pop cycles, [1] cooperative pass cycles, [2] traversal rounds, [3] passes,
-// [4] queue-kernel cycles, [5] closest_coop calls (all summed over waves).
+// Diagnostic build only (-DRT_TIMING=1): wave-clock breakdown of the queue kernels.
+// General kernel: [0] descent + pop cycles, [1] cooperative pass cycles, [2] traversal rounds,
+// [3] passes, [5] closest_coop calls.  Sphere-only kernel: [0] item grab + path start,
+// [1] closest, [2] shade, [3] loop iterations.  [4] queue-kernel cycles (summed over waves).
 __device__ unsigned long long g_rt_timing[8];
 #define RT_CLOCK() __builtin_amdgcn_s_memtime()
 #endif
@@ -1434,8 +1451,12 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     Path p;
 #if RT_TIMING
     const unsigned long long T_start = RT_CLOCK();
+    unsigned long long t_grab = 0, t_closest = 0, t_shade = 0, iters = 0;
 #endif
     for (;;) {
+#if RT_TIMING
+        const unsigned long long T0 = RT_CLOCK();
+#endif
         const uint64_t need = __ballot(!have && !done);
         if (need) {
             const uint32_t n = (uint32_t)__popcll(need);
@@ -1472,13 +1493,39 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
         }
         if (__ballot(have) == 0) {
 #if RT_TIMING
-            if (GEN && lane == 0) atomicAdd(&g_rt_timing[4], RT_CLOCK() - T_start);
+            if (lane == 0) atomicAdd(&g_rt_timing[4], RT_CLOCK() - T_start);
+            if (!GEN && lane == 0) {  // sphere-only kernel: [0] item grab + path start, [1] closest, [2] shade
+                atomicAdd(&g_rt_timing[0], t_grab);
+                atomicAdd(&g_rt_timing[1], t_closest);
+                atomicAdd(&g_rt_timing[2], t_shade);
+                atomicAdd(&g_rt_timing[3], iters);
+            }
 #endif
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
+#if RT_TIMING
+        bool fin;
+        if (!GEN) {
+            const unsigned long long T1 = RT_CLOCK();
+            Hit h;
+            bool hit = false;
+            if (have) hit = closest<false, GEN>(sc, k, p.ray, &h, st, c);
+            const unsigned long long T2 = RT_CLOCK();
+            fin = have && shade<false, GEN, DLS>(sc, k, p, h, hit, c);
+            const unsigned long long T3 = RT_CLOCK();
+            t_grab += T1 - T0;
+            t_closest += T2 - T1;
+            t_shade += T3 - T2;
+            ++iters;
+        } else {
+            fin = (GEN && RT_COOP) ? segment<false, GEN, DLS, GEN && RT_COOP>(sc, k, p, st, c, have) && have
+                                   : have && segment<false, GEN, DLS>(sc, k, p, st, c);
+        }
+#else
         const bool fin = (GEN && RT_COOP) ? segment<false, GEN, DLS, GEN && RT_COOP>(sc, k, p, st, c, have) && have
                                           : have && segment<false, GEN, DLS>(sc, k, p, st, c);
+#endif
         if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;

@@ -29,6 +29,13 @@ def main():
     raw.rt_debug_timing(buf, 1)
     t = list(buf)
     ms = ctx.last_kernel_ms()
+    if loaded.desc.n_free_tris == 0 and loaded.desc.n_meshes == 0 and loaded.desc.n_spheres <= 64:
+        out = {"scene": scene, "spp": spp, "kernel_ms": round(ms, 3), "kernel": "sphere-only",
+               "frac_grab_start": round(t[0] / t[4], 3), "frac_closest": round(t[1] / t[4], 3),
+               "frac_shade": round(t[2] / t[4], 3), "iterations": t[3],
+               "cycles_per_iteration": round(t[4] / max(t[3], 1), 1)}
+        print(json.dumps(out))
+        return
     out = {"scene": scene, "spp": spp, "kernel_ms": round(ms, 3),
            "descent_pop_cycles": t[0], "pass_cycles": t[1], "rounds": t[2], "passes": t[3],
            "queue_cycles": t[4], "closest_calls": t[5]}
