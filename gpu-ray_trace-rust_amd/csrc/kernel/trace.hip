@@ -127,6 +127,20 @@ __device__ __forceinline__ float div_mk(float a, float b, float r) {
     const float q = fmaf(fmaf(-q0, b, a), r, q0);
     return (__float_as_uint(a) << 1) == 0u ? a : q;
 }
+// The Markstein quotient without div_mk's zero test: exact for nonzero a in range; a = +-0
+// gives +0 (callers that need the sign of a zero restore it, or only compare the result).
+__device__ __forceinline__ float div_mk_nz(float a, float b, float r) {
+    const float q0 = a * r;
+    return fmaf(fmaf(-q0, b, a), r, q0);
+}
+// 1.0f / b for a b the caller knows is not below 2^-60 in magnitude (or whose reciprocal it
+// discards otherwise): one compare guards the top of the exact range.
+__device__ __forceinline__ float recip_big(float b) {
+    if (!RT_EXACT_FAST) return 1.0f / b;
+    float r = rcp_exact(b);
+    if (__builtin_expect(!(fabsf(b) < 0x1p60f), 0)) r = 1.0f / b;
+    return r;
+}
 // 1.0f / b, bit for bit
 __device__ __forceinline__ float recip(float b) {
     if (!RT_EXACT_FAST) return 1.0f / b;
@@ -160,6 +174,16 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
     if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
     return s;
 }
+// Cheaper exactness guards (bit-identical either way; A/B on walled in DESIGN.md §8):
+#ifndef RT_G2_NORM
+#define RT_G2_NORM 0        // normalize: copysign instead of div_mk's zero test (-2.5%: off)
+#endif
+#ifndef RT_G2_RCP
+#define RT_G2_RCP 1         // ray_axes / Moller-Trumbore: one-compare guard for reciprocals of |b| >= EPS
+#endif
+#ifndef RT_G2_IRL
+#define RT_G2_IRL 1         // in_return_leaf: no zero test on quotients that are only compared
+#endif
 #ifndef RT_NORM_GUARD
 #define RT_NORM_GUARD 1     // normalize: the Markstein range guard by float compares (see below)
 #endif
@@ -173,7 +197,15 @@ __device__ __forceinline__ V3 normalize(V3 a) {
 #if RT_NORM_GUARD
     if (!RT_EXACT_FAST) return a / n;
     const float r = rcp_exact(n);
+#if RT_G2_NORM
+    // n > 0, so a_i / n has a_i's sign: the Markstein quotient is exact in magnitude (also for
+    // a_i = -0, where it yields +0), and copysign restores the sign — one v_bfi instead of
+    // div_mk's zero test and select.
+    V3 q = mk(copysignf(div_mk_nz(a.x, n, r), a.x), copysignf(div_mk_nz(a.y, n, r), a.y),
+              copysignf(div_mk_nz(a.z, n, r), a.z));
+#else
     V3 q = mk(div_mk(a.x, n, r), div_mk(a.y, n, r), div_mk(a.z, n, r));
+#endif
     if (__builtin_expect(!(mk_range(n) && tiny_ok(a.x) && tiny_ok(a.y) && tiny_ok(a.z)), 0)) q = a / n;
     return q;
 #else
@@ -295,7 +327,11 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
     V3 ray_x_e2 = cross(r.d, e2);
     float det = dot(e1, ray_x_e2);
     if (fabsf(det) < EPS) return false;
+#if RT_G2_RCP
+    float inv_det = recip_big(det);  // |det| >= EPS here
+#else
     float inv_det = recip(det);
+#endif
     V3 rhs = r.o - v0;
     float u = inv_det * dot(rhs, ray_x_e2);
     if (u < 0.0f || u > 1.0f) return false;
@@ -465,9 +501,15 @@ __device__ __forceinline__ RayAx ray_axes(const Ray& r) {
     x.dx = clamp_eps(r.d.x);
     x.dy = clamp_eps(r.d.y);
     x.dz = clamp_eps(r.d.z);
+#if RT_G2_RCP
+    x.rx = recip_big(x.dx);  // clamped: |d| >= EPS (or NaN, which recip_big sends to 1 / d)
+    x.ry = recip_big(x.dy);
+    x.rz = recip_big(x.dz);
+#else
     x.rx = recip(x.dx);
     x.ry = recip(x.dy);
     x.rz = recip(x.dz);
+#endif
     return x;
 }
 // Branch-free pick by axis a in {0,1,2}.
@@ -616,7 +658,12 @@ __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const Ray
         const float d = a == 0 ? ax.dx : (a == 1 ? ax.dy : ax.dz);
         const float rc = a == 0 ? ax.rx : (a == 1 ? ax.ry : ax.rz);
         const float nlo = (c - s.w) - o, nhi = (c + s.w) - o;
+#if RT_G2_IRL
+        // only compared below: the sign of a zero quotient does not matter
+        const float tlo = div_mk_nz(nlo, d, rc), thi = div_mk_nz(nhi, d, rc);
+#else
         const float tlo = div_mk(nlo, d, rc), thi = div_mk(nhi, d, rc);
+#endif
         const float tn = d > 0.0f ? tlo : thi, tf = d > 0.0f ? thi : tlo;
         ok &= mk_num(nlo) && mk_num(nhi);
         ok &= (tn <= e) && (tf > ls);
