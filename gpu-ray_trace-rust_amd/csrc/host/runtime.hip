@@ -49,6 +49,8 @@ struct rt_ctx {
     uint32_t n_cu = 0;
     uint32_t forced_k = 0;        // RT_LANES_PER_PIXEL (tests / tuning)
     uint32_t* d_queue = nullptr;  // queue schedule item counter
+    uint32_t* gstack = nullptr;   // sphere-only queue kernel's traversal stacks (queue_gstack_bytes)
+    size_t gstack_cap = 0;
     int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
     float last_ms = 0.f;
     std::string err;
@@ -118,6 +120,7 @@ static void destroy_ctx(rt_ctx* c) {
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_counts) (void)hipFree(c->d_counts);
     if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->gstack) (void)hipFree(c->gstack);
     if (c->radiance) (void)hipFree(c->radiance);
     for (hipEvent_t e : c->lev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -468,6 +471,7 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
     a->accum = c->accum;
     a->lanes_per_pixel = K;
     a->n_pix = (uint32_t)pix;
+    a->n_pix_magic = pix > 1 ? (uint32_t)((1ull << 32) / pix) : 0u;
     *n_out = pix;
     return RT_OK;
 }
@@ -559,6 +563,17 @@ static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64
         }
         if ((st = ensure_radiance(c, 3 * n_out * chunk))) return st;
         a.radiance = c->radiance;
+        a.gstack = nullptr;
+        if (const size_t gb = queue_gstack_bytes(a, (uint32_t)(lanes / BLOCK))) {
+            if (gb > c->gstack_cap) {
+                if (c->gstack) (void)hipFree(c->gstack);
+                c->gstack = nullptr;
+                c->gstack_cap = 0;
+                if (hipMalloc(&c->gstack, gb) != hipSuccess) return set_err(c, RT_ERR_OOM, "traversal stack alloc failed");
+                c->gstack_cap = gb;
+            }
+            a.gstack = c->gstack;
+        }
         a.queue = c->d_queue;
         uint32_t done = 0;
         do {

@@ -133,12 +133,16 @@ struct LaunchArgs {
     // ([sample][launch pixel] x RGB) and fold_kernel applies the running mean in sample order.
     uint32_t lanes_per_pixel;
     uint32_t n_pix;         // pixels of the launch (tiles concatenated)
+    uint32_t n_pix_magic;   // floor(2^32 / n_pix) (0 for n_pix = 1): item / n_pix by multiply-high
     float* radiance;
     // Queue schedule (launch_trace_queue): persistent lanes take (pixel, sample) items
     // item = j * n_pix + o (sample j of the launch, output pixel o) from *queue in wave-sized
     // grabs, trace them into `radiance` and fold_kernel folds them in sample order.
     uint32_t* queue;
     uint32_t n_items;       // n_pix * sample_count
+    // Sphere-only queue kernel: its traversal stack in global memory, [block][stack_depth][BLOCK]
+    // (queue_gstack_bytes), so the workgroup's LDS holds only the sphere and material tables.
+    uint32_t* gstack;
 };
 
 // Launch wrappers (trace.hip).
@@ -147,5 +151,6 @@ hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_fold(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s);
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks);
+size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks);  // 0: the stack is in LDS
 
 }  // namespace rtd

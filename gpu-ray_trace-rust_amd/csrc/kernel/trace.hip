@@ -175,6 +175,12 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
     return s;
 }
 // Cheaper exactness guards (bit-identical either way; A/B on walled in DESIGN.md §8):
+#ifndef RT_GSTACK
+#define RT_GSTACK 1         // sphere-only queue kernel: traversal stack in global memory (used for 0.05 nodes/sample)
+#endif
+#ifndef RT_LDS_MAT
+#define RT_LDS_MAT 1        // sphere-only kernels: sphere materials read from an LDS table
+#endif
 #ifndef RT_G2_NORM
 #define RT_G2_NORM 0        // normalize: copysign instead of div_mk's zero test (-2.5%: off)
 #endif
@@ -256,6 +262,9 @@ __shared__ uint2 g_lds_nodes[RT_LDS_NODES];
 #if RT_LDS_SPHERES > 0
 __shared__ float4 g_lds_sph[RT_LDS_SPHERES];
 __shared__ float4 g_lds_csq[RT_LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
+#if RT_LDS_MAT
+__shared__ DevMat g_lds_mat[RT_LDS_SPHERES];
+#endif
 #endif
 struct Cache {
     uint32_t n_nodes;  // nodes [0, n_nodes) are in g_lds_nodes
@@ -286,6 +295,9 @@ __device__ __forceinline__ void fill_lds_spheres(const DevScene& sc, Cache& k) {
         const float4 v = sc.sph[i];
         g_lds_sph[i] = v;
         g_lds_csq[i] = make_float4(v.x, v.y, v.z, v.w * v.w);
+#if RT_LDS_MAT
+        g_lds_mat[i] = sc.sph_mat[i];
+#endif
     }
 }
 #endif
@@ -1275,7 +1287,11 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
         V3 perfect = p.ray.o + p.ray.d * h.l;
         n = normalize(perfect - xyz(s));
         pos = perfect + n * EPS;
+#if RT_LDS_MAT && RT_LDS_SPHERES > 0
+        m = GEN ? sc.sph_mat + idx : &g_lds_mat[idx];
+#else
         m = sc.sph_mat + idx;
+#endif
     } else {  // FreeTriangle hit_info (generic.rs:78-92)
         n = xyz(sc.ftri_n[idx - sc.pool_ftri]);
         pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
@@ -1421,6 +1437,17 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     }
 }
 
+// (item / n_pix, item % n_pix) without a 32-bit division: q = mulhi(item, floor(2^32 / n_pix))
+// is floor(item / n_pix) or one less (item < 2^32), and one compare fixes it.
+__device__ __forceinline__ void split_item(const LaunchArgs& a, uint32_t item, uint32_t* j, uint32_t* o) {
+    if (a.n_pix == 1u) { *j = item; *o = 0u; return; }
+    uint32_t q = __umulhi(item, a.n_pix_magic);
+    uint32_t r = item - q * a.n_pix;
+    if (r >= a.n_pix) { ++q; r -= a.n_pix; }
+    *j = q;
+    *o = r;
+}
+
 // Tile holding launch pixel o (tiles are concatenated in out_off order).
 __device__ __forceinline__ uint32_t tile_of(const LaunchArgs& a, uint32_t o) {
     uint32_t lo = 0, hi = a.n_tiles - 1;
@@ -1487,7 +1514,12 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
 #if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
     if (!GEN || RT_LDS_NODES > 0) __syncthreads();
 #endif
+#if RT_GSTACK
+    uint32_t* st = GEN ? dyn_lds + threadIdx.x
+                       : a.gstack + (size_t)blockIdx.x * BLOCK * sc.stack_depth + threadIdx.x;
+#else
     uint32_t* st = dyn_lds + threadIdx.x;
+#endif
     Ctr<false> c;
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
@@ -1520,7 +1552,8 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint32_t item = r < left ? pool + r : base + (r - left);
                 if (item < a.n_items) {
-                    const uint32_t j = item / a.n_pix, o = item - j * a.n_pix;
+                    uint32_t j, o;
+                    split_item(a, item, &j, &o);
                     int x, y;
                     launch_pixel(a, o, &x, &y);
                     start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
@@ -1663,7 +1696,8 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
                 const uint32_t item = rk < left ? pool + rk : base + (rk - left);
                 if (item < a.n_items) {
-                    const uint32_t j = item / a.n_pix, o = item - j * a.n_pix;
+                    uint32_t j, o;
+                    split_item(a, item, &j, &o);
                     int x, y;
                     launch_pixel(a, o, &x, &y);
                     start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
@@ -1841,8 +1875,14 @@ hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks) {
     }
 #endif
     if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true, true>, BLOCK, lds);
-    if (a.sc.spheres_only) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, lds);
+    if (a.sc.spheres_only)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, RT_GSTACK ? 0 : lds);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true>, BLOCK, lds);
+}
+
+size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks) {
+    if (!RT_GSTACK || !a.sc.spheres_only || a.sc.dls) return 0;
+    return (size_t)n_blocks * BLOCK * a.sc.stack_depth * sizeof(uint32_t);
 }
 
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
@@ -1858,7 +1898,7 @@ hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_
     if (a.sc.dls)
         hipLaunchKernelGGL((queue_kernel<true, true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else if (a.sc.spheres_only)
-        hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
+        hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), RT_GSTACK ? 0 : stack_lds_bytes(a), s, a);
     else
         hipLaunchKernelGGL((queue_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
