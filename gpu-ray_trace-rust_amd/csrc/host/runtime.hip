@@ -107,6 +107,10 @@ static DevMat make_mat(const rt_material& m, const float rgb[3]) {
     d.diffp = m.diffp;
     d.n_out = m.n_out;
     d.n_in = m.n_in;
+    d.over_in = m.n_out / m.n_in;
+    d.over_out = m.n_in / m.n_out;
+    const float q = (m.n_out - m.n_in) / (m.n_out + m.n_in);
+    d.r0 = q * q;
     return d;
 }
 

@@ -80,6 +80,28 @@
 #ifndef RT_LDS_SPHERES
 #define RT_LDS_SPHERES 64   // 1 KiB
 #endif
+#ifndef RT_DIVMK_FCMP
+#define RT_DIVMK_FCMP 0     // div_mk's zero test as a float compare (A/B: no difference; off)
+#endif
+#ifndef RT_GSTACK
+#define RT_GSTACK 1         // sphere-only queue kernel: traversal stack in global memory (used for 0.05 nodes/sample)
+#endif
+#ifndef RT_LDS_MAT
+#define RT_LDS_MAT 1        // sphere-only kernels: sphere materials read from an LDS table
+#endif
+// Cheaper exactness guards (bit-identical either way; A/B on walled in DESIGN.md §8):
+#ifndef RT_G2_NORM
+#define RT_G2_NORM 0        // normalize: copysign instead of div_mk's zero test (-2.5%: off)
+#endif
+#ifndef RT_G2_RCP
+#define RT_G2_RCP 1         // ray_axes / Moller-Trumbore: one-compare guard for reciprocals of |b| >= EPS
+#endif
+#ifndef RT_G2_IRL
+#define RT_G2_IRL 1         // in_return_leaf: no zero test on quotients that are only compared
+#endif
+#ifndef RT_NORM_GUARD
+#define RT_NORM_GUARD 1     // normalize: the Markstein range guard by float compares (see below)
+#endif
 
 namespace rtd {
 
@@ -125,7 +147,11 @@ __device__ __forceinline__ float rcp_exact(float b) {
 __device__ __forceinline__ float div_mk(float a, float b, float r) {
     const float q0 = a * r;
     const float q = fmaf(fmaf(-q0, b, a), r, q0);
+#if RT_DIVMK_FCMP
+    return a == 0.0f ? a : q;  // +-0 keeps its sign (one float compare; NaN is not 0)
+#else
     return (__float_as_uint(a) << 1) == 0u ? a : q;
+#endif
 }
 // The Markstein quotient without div_mk's zero test: exact for nonzero a in range; a = +-0
 // gives +0 (callers that need the sign of a zero restore it, or only compare the result).
@@ -174,25 +200,6 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
     if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
     return s;
 }
-// Cheaper exactness guards (bit-identical either way; A/B on walled in DESIGN.md §8):
-#ifndef RT_GSTACK
-#define RT_GSTACK 1         // sphere-only queue kernel: traversal stack in global memory (used for 0.05 nodes/sample)
-#endif
-#ifndef RT_LDS_MAT
-#define RT_LDS_MAT 1        // sphere-only kernels: sphere materials read from an LDS table
-#endif
-#ifndef RT_G2_NORM
-#define RT_G2_NORM 0        // normalize: copysign instead of div_mk's zero test (-2.5%: off)
-#endif
-#ifndef RT_G2_RCP
-#define RT_G2_RCP 1         // ray_axes / Moller-Trumbore: one-compare guard for reciprocals of |b| >= EPS
-#endif
-#ifndef RT_G2_IRL
-#define RT_G2_IRL 1         // in_return_leaf: no zero test on quotients that are only compared
-#endif
-#ifndef RT_NORM_GUARD
-#define RT_NORM_GUARD 1     // normalize: the Markstein range guard by float compares (see below)
-#endif
 // nalgebra normalize: a / |a| per component.  div3's guard, specialised: |a_i| < 2^60 follows
 // from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs
 // "zero or |a_i| >= 2^-60" — one compare with a free abs modifier and one equality.  A NaN
@@ -1041,20 +1048,19 @@ __device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
     float y = r * sn;
     return normalize((xd * x + yd * y) + n * sqrt_nonneg(fmaxf(1.0f - u, 0.0f)));
 }
-__device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float n_out, float n_in, float* p,
+// over_in = n_out / n_in, over_out = n_in / n_out and r0 come precomputed (DevMat): the
+// divisions n1 / n2 and (n1 - n2) / (n1 + n2) of :35,48 depend on the material only.
+__device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float over_in, float over_out, float r0, float* p,
                                           uint32_t* rng) {  // :29-59
     float c_ = dot(n, d);
     bool into = c_ < 0.0f;
-    float n1 = into ? n_out : n_in, n2 = into ? n_in : n_out;
     float c1 = into ? -c_ : c_;
     V3 norm_refr = into ? n : -n;
-    float n_over = n1 / n2;
+    float n_over = into ? over_in : over_out;
     float c22 = 1.0f - n_over * n_over * (1.0f - c1 * c1);
     V3 refl = spec_dir(d, norm_refr);
     if (c22 < 0.0f) { *p = 1.0f; return refl; }
     V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrt_nonneg(c22));  // c22 >= 0 here
-    float q = (n1 - n2) / (n1 + n2);
-    float r0 = q * q;
     float c = 1.0f - (into ? c1 : dot(trns, n));
     float re = r0 + (1.0f + r0) * rt_powf5(c);  // glibc's powf(c, 5)
     float u = draw(rng);
@@ -1312,7 +1318,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
     if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
         nd = spec_dir(p.ray.d, n);
     } else if (divert == RT_DIVERT_DIELECTRIC) {
-        nd = refract_dir(p.ray.d, n, m->n_out, m->n_in, &prob, &p.rng);
+        nd = refract_dir(p.ray.d, n, m->over_in, m->over_out, m->r0, &prob, &p.rng);
     } else {
         nd = diff_dir(p.ray.d, n, &p.rng);
     }
