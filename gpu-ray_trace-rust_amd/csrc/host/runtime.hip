@@ -111,6 +111,7 @@ static DevMat make_mat(const rt_material& m, const float rgb[3]) {
     d.over_out = m.n_in / m.n_out;
     const float q = (m.n_out - m.n_in) / (m.n_out + m.n_in);
     d.r0 = q * q;
+    for (int i = 0; i < 3; ++i) d.rgb_atten[i] = d.rgb[i] / 0.4f;  // RR_THRES
     return d;
 }
 

@@ -20,7 +20,7 @@ constexpr uint32_t REF_KIND_SHIFT = 30;
 constexpr uint32_t REF_INDEX_MASK = (1u << 30) - 1u;
 enum : uint32_t { K_SPHERE = 0, K_FREE_TRI = 1, K_MESH_TRI = 2 };
 
-// Shading record of a sphere / free triangle (UniformDiffuseSpec + Coloring).  56 bytes.
+// Shading record of a sphere / free triangle (UniformDiffuseSpec + Coloring).  72 bytes.
 struct DevMat {
     float rgb[3];
     float em[3];       // zero when the material has no emissive (sphere.rs:70-75)
@@ -31,7 +31,8 @@ struct DevMat {
     // same f32 operations: n_out / n_in, n_in / n_out, and r0 = q * q with
     // q = (n1 - n2) / (n1 + n2) — the same value entering or leaving (q changes sign only).
     float over_in, over_out, r0;
-    uint32_t _pad;
+    float rgb_atten[3];  // rgb / 0.4 (radiance.rs:44's 1/atten with p = 1), same f32 division
+    uint32_t _pad[2];
 };
 
 struct DevFace {       // one DistantCubeMap face: texel offset, size, uv scales

@@ -1323,7 +1323,8 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
         nd = diff_dir(p.ray.d, n, &p.rng);
     }
     V3 rgb = ld3(m->rgb) * prob;
-    if (atten) rgb = div3(rgb, RR_THRES);
+    // rgb * 1 is rgb, so with p = 1 the attenuated colour is the host's rgb / 0.4
+    if (atten) rgb = prob == 1.0f ? ld3(m->rgb_atten) : div3(rgb, RR_THRES);
     p.T = cmul(p.T, rgb);
     p.ray.d = nd;
     p.ray.o = pos;
