@@ -62,6 +62,9 @@
 #ifndef RT_TIMING
 #define RT_TIMING 0         // diagnostic build: wave-clock breakdown (rt_debug_timing), never the product
 #endif
+#ifndef RT_COOP_DELTA
+#define RT_COOP_DELTA 1     // cooperative passes: one shuffle of (off - start) instead of three
+#endif
 #ifndef RT_OWNER_SCAN
 #define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
 #endif
@@ -850,6 +853,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 }
 
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
+// Returns the lane's leaf minimum as (bits(l) << 32 | index into sc.refs), ~0 for none; one
+// leaf's refs are contiguous, so the index orders like the position in the leaf.
 __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
                                                         uint32_t cnt, uint32_t lane) {
 #if RT_COOP
@@ -883,20 +888,25 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             owner += e <= w ? step : 0u;
         }
 #endif
+#if RT_COOP_DELTA
+        // item w of the owner's leaf is sc.refs[w + (off - start)] of the owner: one shuffle
+        const uint32_t idx = w + __shfl(off - (incl - cnt), owner);
+#else
         const uint32_t o_end = __shfl(incl, owner), o_cnt = __shfl(cnt, owner), o_off = __shfl(off, owner);
+        const uint32_t idx = o_off + (w - (o_end - o_cnt));
+#endif
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
         if (w < total) {
-            const uint32_t pos = w - (o_end - o_cnt);
-            const uint32_t ref = sc.refs[o_off + pos];
+            const uint32_t ref = sc.refs[idx];
             const float4* pd = prim_data(sc, ref);
             float l = 0.f, bu, bv;
             bool h;
             if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(pd[0], ro, &l);
             else h = tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), ro, &l, &bu, &bv);
             if (h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | pos);
+                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
         }
     }
     return __hip_atomic_load(&g_coop_key[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -958,7 +968,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
         if (!done) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
-                const uint32_t ref = sc.refs[off + (uint32_t)key];
+                const uint32_t ref = sc.refs[(uint32_t)key];
                 const float4* pd = prim_data(sc, ref);
                 float l = 0.f, bu = 0.f, bv = 0.f;
                 if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(pd[0], r, &l);
@@ -1759,7 +1769,7 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
         if (tr) {
             bool ret = false;
             if (key != ~0ull) {
-                const uint32_t ref = sc.refs[off + (uint32_t)key];
+                const uint32_t ref = sc.refs[(uint32_t)key];
                 const float4* pd = prim_data(sc, ref);
                 float l = 0.f, bu = 0.f, bv = 0.f;
                 if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(pd[0], p.ray, &l);
