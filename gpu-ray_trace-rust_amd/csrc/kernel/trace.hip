@@ -65,6 +65,9 @@
 #ifndef RT_COOP_DELTA
 #define RT_COOP_DELTA 1     // cooperative passes: one shuffle of (off - start) instead of three
 #endif
+#ifndef RT_OWNER_NARROW
+#define RT_OWNER_NARROW 0   // coop passes: search only the owners ending inside the pass (biplane +3%, a380 -1.5%: off)
+#endif
 #ifndef RT_OWNER_SCAN
 #define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
 #endif
@@ -880,6 +883,17 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                                __HIP_MEMORY_SCOPE_WAVEFRONT);
         const uint32_t owner =
             wave_incl_max(__hip_atomic_load(&g_coop_slot[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) - 1u;
+#elif RT_OWNER_NARROW
+        // The owner of item w is the number of lanes whose inclusive end is <= w.  Lanes ending at
+        // or before the pass start are counted by one ballot; only the n lanes that end inside
+        // the pass remain to be searched, in ceil(log2(n + 1)) shuffle steps (wave-uniform) instead
+        // of 6 — lanes past them end after the pass, so the search never runs beyond them.
+        uint32_t owner = (uint32_t)__popcll(__ballot(incl <= base));
+        const uint32_t n_in = (uint32_t)__popcll(__ballot(incl > base && incl < base + 64u));
+        for (uint32_t step = n_in ? 1u << (31 - __builtin_clz(n_in)) : 0u; step; step >>= 1) {
+            const uint32_t e = __shfl(incl, min(owner + step - 1, 63u));  // lane 63 ends at total > w
+            owner += e <= w ? step : 0u;
+        }
 #else
         uint32_t owner = 0;  // lanes whose inclusive end is <= w
 #pragma unroll
