@@ -35,3 +35,10 @@ def test_libm_restatement_matches_glibc_cpu():
 def test_libm_restatement_matches_glibc_on_gfx950(gpu_available):
     r = _run("check_libm_gpu", timeout=120)
     assert r["angles_2pi_v"][1] == 0 and r["hashed_pm2pi"][1] == 0 and r["powf5"][1] == 0, r
+
+
+def test_libm_restatement_exhaustive_cpu():
+    """Every float in [-2 pi, 2 pi] (sinf, cosf) and in [0, 1.001] / [-0.001, 0] (powf(x, 5)):
+    4.2e9 inputs, bit for bit (about 10 s on 8 cores)."""
+    r = _run("check_libm", "full", timeout=600)
+    assert r["sincos_all_floats_pm2pi"][1] == 0 and r["powf5_all_floats"][1] == 0, r
