@@ -1056,10 +1056,14 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Cache& k,
 // ---------------------------------------------------------------- materials (interaction.rs)
 __device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rng); }
 
-__device__ __forceinline__ V3 spec_dir(V3 d, V3 n) {  // :6-9
-    return normalize(d - (n * 2.0f) * dot(d, n));
+// Every continued direction of interaction.rs ends in a normalize.  The *_vec functions return
+// the vector before it, so shade() normalizes once, after the material branches: a wave whose
+// lanes hit diffuse, mirror and glass spheres runs one normalize at full width instead of one
+// per branch at partial width.  Each lane still normalizes exactly the vector the reference does.
+__device__ __forceinline__ V3 spec_vec(V3 d, V3 n) {  // :6-9
+    return d - (n * 2.0f) * dot(d, n);
 }
-__device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
+__device__ __forceinline__ V3 diff_vec(V3 d, V3 n, uint32_t* rng) {  // :11-27
     V3 xd = normalize(d - n * dot(d, n));
     V3 yd = normalize(cross(n, xd));
     float u = draw(rng);
@@ -1070,11 +1074,13 @@ __device__ __forceinline__ V3 diff_dir(V3 d, V3 n, uint32_t* rng) {  // :11-27
     (void)rt_sincosf(thet, &sn, &cs);  // glibc's sinf, cosf (rt_libm.h); thet in [0, 2 pi)
     float x = r * cs;
     float y = r * sn;
-    return normalize((xd * x + yd * y) + n * sqrt_nonneg(fmaxf(1.0f - u, 0.0f)));
+    // max(1 - u, 0) is 1 - u: u <= 1 - 2^-24
+    return (xd * x + yd * y) + n * sqrt_nonneg(1.0f - u);
 }
 // over_in = n_out / n_in, over_out = n_in / n_out and r0 come precomputed (DevMat): the
 // divisions n1 / n2 and (n1 - n2) / (n1 + n2) of :35,48 depend on the material only.
-__device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float over_in, float over_out, float r0, float* p,
+// Returns the reflected (spec_vec) or transmitted vector, to be normalized by the caller.
+__device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float over_in, float over_out, float r0, float* p,
                                           uint32_t* rng) {  // :29-59
     float c_ = dot(n, d);
     bool into = c_ < 0.0f;
@@ -1082,7 +1088,7 @@ __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float over_in, float over_
     V3 norm_refr = into ? n : -n;
     float n_over = into ? over_in : over_out;
     float c22 = 1.0f - n_over * n_over * (1.0f - c1 * c1);
-    V3 refl = spec_dir(d, norm_refr);
+    const V3 refl = spec_vec(d, norm_refr);
     if (c22 < 0.0f) { *p = 1.0f; return refl; }
     V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrt_nonneg(c22));  // c22 >= 0 here
     float c = 1.0f - (into ? c1 : dot(trns, n));
@@ -1090,7 +1096,7 @@ __device__ __forceinline__ V3 refract_dir(V3 d, V3 n, float over_in, float over_
     float u = draw(rng);
     if (u < re) { *p = re; return refl; }
     *p = 1.0f - re;
-    return normalize(trns);
+    return trns;
 }
 
 // UVRgb32FImage::get_pixel (uv_image.rs:9-23): nearest texel, clamped, truncated; `as u32`
@@ -1273,7 +1279,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
         if (!(draw(&p.rng) < RR_THRES)) return true;
         atten = true;
     }
-    V3 nd = should_diff ? diff_dir(p.ray.d, n, &p.rng) : spec_dir(p.ray.d, n);  // divert_new_ray
+    V3 nd = normalize(should_diff ? diff_vec(p.ray.d, n, &p.rng) : spec_vec(p.ray.d, n));  // divert_new_ray
     const float su = draw(&p.rng), sv = draw(&p.rng), sw = draw(&p.rng);
     const V3 scatter = rough * normalize(mk(su, sv, sw));
     nd = normalize(nd + scatter);
@@ -1340,12 +1346,13 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
     float prob = 1.0f;  // gen_new_ray (uniform_diff_spec.rs:44-68)
     V3 nd;
     if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
-        nd = spec_dir(p.ray.d, n);
+        nd = spec_vec(p.ray.d, n);
     } else if (divert == RT_DIVERT_DIELECTRIC) {
-        nd = refract_dir(p.ray.d, n, m->over_in, m->over_out, m->r0, &prob, &p.rng);
+        nd = refract_vec(p.ray.d, n, m->over_in, m->over_out, m->r0, &prob, &p.rng);
     } else {
-        nd = diff_dir(p.ray.d, n, &p.rng);
+        nd = diff_vec(p.ray.d, n, &p.rng);
     }
+    nd = normalize(nd);
     V3 rgb = ld3(m->rgb) * prob;
     // rgb * 1 is rgb, so with p = 1 the attenuated colour is the host's rgb / 0.4
     if (atten) rgb = prob == 1.0f ? ld3(m->rgb_atten) : div3(rgb, RR_THRES);
