@@ -1056,10 +1056,11 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Cache& k,
 // ---------------------------------------------------------------- materials (interaction.rs)
 __device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rng); }
 
-// Every continued direction of interaction.rs ends in a normalize.  The *_vec functions return
-// the vector before it, so shade() normalizes once, after the material branches: a wave whose
-// lanes hit diffuse, mirror and glass spheres runs one normalize at full width instead of one
-// per branch at partial width.  Each lane still normalizes exactly the vector the reference does.
+// Every continued direction of interaction.rs ends in a normalize, and so does the camera ray.
+// The *_vec functions return the vector before it, and segment() normalizes once at its start:
+// a wave whose lanes hit diffuse, mirror and glass spheres, or start new paths, runs one
+// normalize at full width instead of one per branch at partial width.  Each lane still
+// normalizes exactly the vector the reference does.
 __device__ __forceinline__ V3 spec_vec(V3 d, V3 n) {  // :6-9
     return d - (n * 2.0f) * dot(d, n);
 }
@@ -1162,8 +1163,7 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint
     float u = draw(rng) - 0.5f;
     float v = draw(rng) - 0.5f;
     ray.d = (ray.d + (right * u) * sc.x_cf) + (up * v) * sc.y_cf;
-    ray.d = normalize(ray.d);
-    return ray;
+    return ray;  // d not yet normalized: segment() normalizes it (generate.rs:63)
 }
 
 // ---------------------------------------------------------------- one path segment (radiance.rs)
@@ -1282,7 +1282,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
     V3 nd = normalize(should_diff ? diff_vec(p.ray.d, n, &p.rng) : spec_vec(p.ray.d, n));  // divert_new_ray
     const float su = draw(&p.rng), sv = draw(&p.rng), sw = draw(&p.rng);
     const V3 scatter = rough * normalize(mk(su, sv, sw));
-    nd = normalize(nd + scatter);
+    nd = nd + scatter;  // normalized at the start of the next segment
     V3 rgb = mk(pr.base_factor[0], pr.base_factor[1], pr.base_factor[2]);  // RgbFromMesh (:166-178)
     if (pr.base_tex >= 0) {
         float u, v;
@@ -1352,7 +1352,6 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
     } else {
         nd = diff_vec(p.ray.d, n, &p.rng);
     }
-    nd = normalize(nd);
     V3 rgb = ld3(m->rgb) * prob;
     // rgb * 1 is rgb, so with p = 1 the attenuated colour is the host's rgb / 0.4
     if (atten) rgb = prob == 1.0f ? ld3(m->rgb_atten) : div3(rgb, RR_THRES);
@@ -1374,6 +1373,10 @@ template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true) {
     if (COUNT) c.segments++;
+    // The ray's direction arrives un-normalized from camera_ray or shade: one normalize here
+    // serves a wave's new paths and continued ones alike (each lane normalizes the same vector
+    // the reference does, just later).
+    p.ray.d = normalize(p.ray.d);
     Hit h;
     const bool hit = COOP ? closest_coop(sc, k, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
     if (COOP && !active) return false;
@@ -1758,6 +1761,7 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
 
         bool resolved = false, hit = false;
         Hit h;
+        if (need) p.ray.d = normalize(p.ray.d);  // arrives un-normalized (see segment())
         const RayAx ax = ray_axes(p.ray);
         if (need) {  // a new traversal: root slab test (kdtree.rs:59-61)
             need = false;
