@@ -1057,15 +1057,13 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Cache& k,
 __device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rng); }
 
 // Every continued direction of interaction.rs ends in a normalize, and so does the camera ray.
-// The *_vec functions return the vector before it, and segment() normalizes once at its start:
+// The *_vec functions (and the mirror direction, computed inline) return the vector before it, and segment() normalizes once at its start:
 // a wave whose lanes hit diffuse, mirror and glass spheres, or start new paths, runs one
 // normalize at full width instead of one per branch at partial width.  Each lane still
 // normalizes exactly the vector the reference does.
-__device__ __forceinline__ V3 spec_vec(V3 d, V3 n) {  // :6-9
-    return d - (n * 2.0f) * dot(d, n);
-}
-__device__ __forceinline__ V3 diff_vec(V3 d, V3 n, uint32_t* rng) {  // :11-27
-    V3 xd = normalize(d - n * dot(d, n));
+// dn = dot(d, n), shared by the callers' branches
+__device__ __forceinline__ V3 diff_vec(V3 d, V3 n, float dn, uint32_t* rng) {  // :11-27
+    V3 xd = normalize(d - n * dn);
     V3 yd = normalize(cross(n, xd));
     float u = draw(rng);
     float v = draw(rng);
@@ -1080,16 +1078,18 @@ __device__ __forceinline__ V3 diff_vec(V3 d, V3 n, uint32_t* rng) {  // :11-27
 }
 // over_in = n_out / n_in, over_out = n_in / n_out and r0 come precomputed (DevMat): the
 // divisions n1 / n2 and (n1 - n2) / (n1 + n2) of :35,48 depend on the material only.
-// Returns the reflected (spec_vec) or transmitted vector, to be normalized by the caller.
-__device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float over_in, float over_out, float r0, float* p,
-                                          uint32_t* rng) {  // :29-59
-    float c_ = dot(n, d);
+// Returns the reflected or transmitted vector, to be normalized by the caller.
+// dn = dot(d, n) (= dot(n, d): products commute) and refl = d - 2n(d.n), the mirror direction
+// of :6-9, come from the caller; the mirror about -n is the same vector bit for bit (each
+// negation is exact).
+__device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float dn, V3 refl, float over_in, float over_out,
+                                          float r0, float* p, uint32_t* rng) {  // :29-59
+    float c_ = dn;
     bool into = c_ < 0.0f;
     float c1 = into ? -c_ : c_;
     V3 norm_refr = into ? n : -n;
     float n_over = into ? over_in : over_out;
     float c22 = 1.0f - n_over * n_over * (1.0f - c1 * c1);
-    const V3 refl = spec_vec(d, norm_refr);
     if (c22 < 0.0f) { *p = 1.0f; return refl; }
     V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrt_nonneg(c22));  // c22 >= 0 here
     float c = 1.0f - (into ? c1 : dot(trns, n));
@@ -1279,7 +1279,8 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
         if (!(draw(&p.rng) < RR_THRES)) return true;
         atten = true;
     }
-    V3 nd = normalize(should_diff ? diff_vec(p.ray.d, n, &p.rng) : spec_vec(p.ray.d, n));  // divert_new_ray
+    const float dn = dot(p.ray.d, n);
+    V3 nd = normalize(should_diff ? diff_vec(p.ray.d, n, dn, &p.rng) : p.ray.d - (n * 2.0f) * dn);  // divert_new_ray
     const float su = draw(&p.rng), sv = draw(&p.rng), sw = draw(&p.rng);
     const V3 scatter = rough * normalize(mk(su, sv, sw));
     nd = nd + scatter;  // normalized at the start of the next segment
@@ -1344,13 +1345,16 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
         atten = true;
     }
     float prob = 1.0f;  // gen_new_ray (uniform_diff_spec.rs:44-68)
+    // d.n and the mirror direction are shared by the three branches (computed once, full width)
+    const float dn = dot(p.ray.d, n);
+    const V3 refl = p.ray.d - (n * 2.0f) * dn;  // spec (interaction.rs:6-9)
     V3 nd;
     if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
-        nd = spec_vec(p.ray.d, n);
+        nd = refl;
     } else if (divert == RT_DIVERT_DIELECTRIC) {
-        nd = refract_vec(p.ray.d, n, m->over_in, m->over_out, m->r0, &prob, &p.rng);
+        nd = refract_vec(p.ray.d, n, dn, refl, m->over_in, m->over_out, m->r0, &prob, &p.rng);
     } else {
-        nd = diff_vec(p.ray.d, n, &p.rng);
+        nd = diff_vec(p.ray.d, n, dn, &p.rng);
     }
     V3 rgb = ld3(m->rgb) * prob;
     // rgb * 1 is rgb, so with p = 1 the attenuated colour is the host's rgb / 0.4
