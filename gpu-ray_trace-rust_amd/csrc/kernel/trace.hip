@@ -1635,7 +1635,10 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
             const unsigned long long T1 = RT_CLOCK();
             Hit h;
             bool hit = false;
-            if (have) hit = closest<false, GEN>(sc, k, p.ray, &h, st, c);
+            if (have) {
+                p.ray.d = normalize(p.ray.d);  // as segment() does
+                hit = closest<false, GEN>(sc, k, p.ray, &h, st, c);
+            }
             const unsigned long long T2 = RT_CLOCK();
             fin = have && shade<false, GEN, DLS>(sc, k, p, h, hit, c);
             const unsigned long long T3 = RT_CLOCK();
