@@ -1,4 +1,4 @@
-"""Copies the reference's own CPU-path renders (info/images_cpu_comparison/{walled,biplane}.png,
+"""Copies the reference's own CPU-path renders (info/images_cpu_comparison/{walled,biplane,spaceship_r1}.png,
 README.md:177-194: the CPU renderer run for as long as the GPU took) into
 tests/golden/ref_cpu_images.npz as RGB u8 arrays, exactly as stored (the PNG writer's flipped
 orientation).  They are outputs of the reference itself, used as a statistical anchor of the
@@ -16,7 +16,7 @@ SRC = "/root/reference/info/images_cpu_comparison"
 
 def main():
     out = {}
-    for name in ("walled", "biplane"):
+    for name in ("walled", "biplane", "spaceship_r1"):
         im = Image.open(os.path.join(SRC, name + ".png")).convert("RGB")
         out[name] = np.asarray(im, dtype=np.uint8)
         print(name, out[name].shape)

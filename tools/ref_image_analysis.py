@@ -36,7 +36,7 @@ def main():
     sc = load_scene(scene)
     w, h = int(sc.info.width), int(sc.info.height)
     print(json.dumps({"ref_noise": noise(ref), "ref_mean": float(ref.mean())}))
-    spps = [2, 4, 6, 8, 10, 12, 16, 24] if scene == "walled" else [1, 2, 3, 4, 6, 8, 12]
+    spps = [2, 4, 6, 8, 10, 12, 16, 24] if scene == "walled" else [1, 2, 3, 4, 6, 8, 12, 16, 24]
     for spp in spps:
         imgs = []
         for seed in range(4):
