@@ -96,6 +96,9 @@
 #define RT_LDS_MAT 1        // sphere-only kernels: sphere materials read from an LDS table
 #endif
 // Cheaper exactness guards (bit-identical either way; A/B on walled in DESIGN.md §8):
+#ifndef RT_NORM_MIN3
+#define RT_NORM_MIN3 1      // normalize: one min3 guard; zero / tiny components take the IEEE division
+#endif
 #ifndef RT_G2_NORM
 #define RT_G2_NORM 0        // normalize: copysign instead of div_mk's zero test (-2.5%: off)
 #endif
@@ -216,7 +219,15 @@ __device__ __forceinline__ V3 normalize(V3 a) {
 #if RT_NORM_GUARD
     if (!RT_EXACT_FAST) return a / n;
     const float r = rcp_exact(n);
-#if RT_G2_NORM
+#if RT_NORM_MIN3
+    // Common case: every |a_i| >= 2^-60 (one v_min3 and one compare), so no numerator is zero
+    // and div_mk's zero test is not needed either.  A zero or tiny component, or n out of range,
+    // takes the IEEE division (a divergent branch that lanes rarely take).
+    V3 q = mk(div_mk_nz(a.x, n, r), div_mk_nz(a.y, n, r), div_mk_nz(a.z, n, r));
+    const float amin = fminf(fminf(fabsf(a.x), fabsf(a.y)), fabsf(a.z));
+    if (__builtin_expect(!(mk_range(n) && amin >= 0x1p-60f), 0)) q = a / n;
+    return q;
+#elif RT_G2_NORM
     // n > 0, so a_i / n has a_i's sign: the Markstein quotient is exact in magnitude (also for
     // a_i = -0, where it yields +0), and copysign restores the sign — one v_bfi instead of
     // div_mk's zero test and select.
