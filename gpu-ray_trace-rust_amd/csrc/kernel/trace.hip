@@ -71,6 +71,9 @@
 #ifndef RT_OWNER_SCAN
 #define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
 #endif
+#ifndef RT_SPH_PAIRS
+#define RT_SPH_PAIRS 1      // closest_small: discriminants of two spheres at a time (4: four, no further gain)
+#endif
 #ifndef RT_SPH_PREFETCH
 #define RT_SPH_PREFETCH 0   // closest_small: next sphere's LDS record read ahead of the current test
 #endif
@@ -729,6 +732,41 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
 #if RT_SPH_PREFETCH
     float4 sq_next = g_lds_csq[0];
 #endif
+#if RT_SPH_PAIRS
+    // Spheres in pairs: the two discriminants are independent, so their arithmetic interleaves
+    // (the per-sphere skip branch keeps the compiler from overlapping consecutive iterations).
+    auto take = [&](const SphDisc& q, uint32_t i) {
+        if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) return;  // v false on every lane
+        float l;
+        const bool v = sphere_roots(q, &l) & !(l < HIT_MIN);
+        any |= v;
+        const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
+        imin = better ? i : imin;
+        ls = better ? l : ls;
+    };
+    uint32_t i = 0;
+#if RT_SPH_PAIRS >= 4
+    for (; i + 3 < sc.n_spheres; i += 4) {
+        const float4 sa = g_lds_csq[i], sb = g_lds_csq[i + 1], sc2 = g_lds_csq[i + 2], sd = g_lds_csq[i + 3];
+        const SphDisc qa = sphere_disc(sa, sa.w, r), qb = sphere_disc(sb, sb.w, r);
+        const SphDisc qc = sphere_disc(sc2, sc2.w, r), qd = sphere_disc(sd, sd.w, r);
+        take(qa, i);
+        take(qb, i + 1);
+        take(qc, i + 2);
+        take(qd, i + 3);
+    }
+#endif
+    for (; i + 1 < sc.n_spheres; i += 2) {
+        const float4 sa = g_lds_csq[i], sb = g_lds_csq[i + 1];
+        const SphDisc qa = sphere_disc(sa, sa.w, r), qb = sphere_disc(sb, sb.w, r);
+        take(qa, i);
+        take(qb, i + 1);
+    }
+    if (i < sc.n_spheres) {
+        const float4 sa = g_lds_csq[i];
+        take(sphere_disc(sa, sa.w, r), i);
+    }
+#else
 #pragma unroll RT_SPH_UNROLL
     for (uint32_t i = 0; i < sc.n_spheres; ++i) {
 #if RT_SPH_PREFETCH
@@ -746,6 +784,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
         imin = better ? i : imin;
         ls = better ? l : ls;
     }
+#endif
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (any && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
