@@ -269,3 +269,20 @@ def test_small_scene_closest_sphere_bit_exact(gpu_available, oracle, seed):
         g = c.render(tiles, 0, 3)
     o = oracle.render(sc, tiles, 0, 3)
     assert np.array_equal(g, o), parity.stats(g, o)
+
+
+def test_wide_frame_without_pixel_table(gpu_available, oracle):
+    """A frame over 65535 pixels wide cannot use the packed (y << 16 | x) pixel table
+    (runtime.hip prepare_tiles): the kernels fall back to the binary search over the tiles.
+    Both paths must give the oracle's pixels, for one tile and for several."""
+    from rt_amd import render
+
+    sc = load_scene("walled", width=70000, height=3)
+    tiles = [(0, 0, 40, 1), (69990, 2, 10, 1), (35000, 1, 33, 2)]
+    with render.Context(sc) as c:
+        g = c.render(tiles, 0, 4)
+        g1 = c.render([(34990, 0, 64, 3)], 0, 4)
+    o = oracle.render(sc, tiles, 0, 4, accum=oracle.ACCUM_FORWARD)
+    o1 = oracle.render(sc, [(34990, 0, 64, 3)], 0, 4, accum=oracle.ACCUM_FORWARD)
+    assert np.array_equal(g, o), parity.stats(g, o)
+    assert np.array_equal(g1, o1), parity.stats(g1, o1)
