@@ -104,8 +104,16 @@ def cpu_baseline(loaded, target_s=10.0, threads=None):
         per = max(timed(2) - t1, 0.05 * t1)
         spp = max(1, min(256, int(round((target_s - (t1 - per)) / per))))
         dt = timed(spp)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": f"full {w}x{h} frame, {spp} spp in one call (KD build included, as per frame in "
                       f"the reference), oracle/oracle.cpp recursive radiance, {threads} threads, {dt:.1f} s"}
 
