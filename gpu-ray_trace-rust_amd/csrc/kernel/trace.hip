@@ -80,6 +80,12 @@
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
+#ifndef RT_REGEN_MIN
+#define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
+#endif
+#ifndef RT_REGEN_MIN_GEN
+#define RT_REGEN_MIN_GEN 1  // the same for the general queue kernel (16-40: no gain on the mesh scenes)
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
@@ -1632,7 +1638,10 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
         const unsigned long long T0 = RT_CLOCK();
 #endif
         const uint64_t need = __ballot(!have && !done);
-        if (need) {
+        // Starting paths is wave-wide work at the width of the idle lanes: in the sphere-only
+        // kernel ~10 of 64 lanes end a path per segment, so it waits for RT_REGEN_MIN of them.
+        constexpr int regen_min = GEN ? RT_REGEN_MIN_GEN : RT_REGEN_MIN;
+        if (need && (regen_min <= 1 || __popcll(need) >= regen_min || __ballot(have) == 0)) {
             const uint32_t n = (uint32_t)__popcll(need);
             const uint32_t left = pool_end - pool;
             uint32_t base = pool_end;
