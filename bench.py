@@ -118,6 +118,24 @@ def cpu_baseline(loaded, target_s=10.0, threads=None):
                       f"the reference), oracle/oracle.cpp recursive radiance, {threads} threads, {dt:.1f} s"}
 
 
+def measured_valu_stream():
+    """G wave-instructions/s of a pure full-rate VALU stream (v_fma_f32, distinct operands) from
+    the committed tools/valu_rates.hip run (profiles/*_valu_rates.json), or None.  Under a full
+    VALU load the chip does not hold 2.4 GHz, so this is the ceiling actually reachable."""
+    import glob
+
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_rates.json"))):
+        try:
+            rows = [json.loads(line) for line in open(p) if line.strip()]
+        except (OSError, ValueError):
+            continue
+        for r in rows:
+            if r.get("insn") == "v_fma_f32":
+                best = (r["G_winst_per_s"], os.path.relpath(p, ROOT))
+    return best
+
+
 def valu_roofline(scene, samples_per_launch, kernel_ms):
     """The bound the kernel actually runs against: VALU instruction issue."""
     c = committed_valu(scene, samples_per_launch)
@@ -125,9 +143,15 @@ def valu_roofline(scene, samples_per_launch, kernel_ms):
         return None
     d, src = c
     rate = d["valu_insts_per_launch"] / (kernel_ms * 1e-3)
-    return {"insts_per_launch": d["valu_insts_per_launch"], "achieved_winst_per_s": round(rate / 1e9, 1),
-            "peak_winst_per_s": round(VALU_PEAK_WINST_S / 1e9, 1), "unit": "G wave-instructions/s",
-            "frac": round(rate / VALU_PEAK_WINST_S, 4), "lane_util": d.get("valu_lane_util"), "source": src}
+    out = {"insts_per_launch": d["valu_insts_per_launch"], "achieved_winst_per_s": round(rate / 1e9, 1),
+           "peak_winst_per_s": round(VALU_PEAK_WINST_S / 1e9, 1), "unit": "G wave-instructions/s",
+           "frac": round(rate / VALU_PEAK_WINST_S, 4), "lane_util": d.get("valu_lane_util"), "source": src}
+    m = measured_valu_stream()
+    if m:
+        out["measured_stream_winst_per_s"] = m[0]
+        out["frac_of_measured_stream"] = round(rate / 1e9 / m[0], 4)
+        out["measured_stream_source"] = m[1]
+    return out
 
 
 def main():
