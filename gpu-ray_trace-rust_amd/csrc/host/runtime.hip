@@ -343,6 +343,24 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         if (m != 0u && (m < (57u << 23) || m >= (188u << 23))) d.fastdiv = 0;
     }
     d.stack_depth = tree->max_leaf_depth ? tree->max_leaf_depth : 1u;
+    // closest_small (trace.hip) relies on finite sphere roots: every ray origin (camera, lens
+    // point, or a point on a sphere) then has |o_i| < 2^59, so |o - c| < 2^60 per component and
+    // dot(d, o - c), (o - c).(o - c) - r^2 and the discriminant stay finite for unit d.
+    {
+        const float lim = 0x1p58f;
+        bool ok = true;
+        for (uint32_t i = 0; i < scene->n_spheres && ok; ++i) {
+            const rt_sphere& sp = scene->spheres[i];
+            for (int a = 0; a < 3; ++a) ok = ok && std::fabs(sp.c[a]) + std::fabs(sp.r) < lim;
+        }
+        float up2 = 0.f;
+        for (int a = 0; a < 3; ++a) {
+            ok = ok && std::fabs(cam->o[a]) < lim;
+            up2 += cam->up[a] * cam->up[a];
+        }
+        ok = ok && (!cam->has_lens || std::fabs(cam->lens_r) * (std::sqrt(up2) + 2.0f) < lim);
+        d.small_ok = ok ? 1u : 0u;
+    }
     d.n_spheres = scene->n_spheres;
     // the sphere-only kernel reads every sphere from its LDS table (trace.hip fetch_sphere)
     // (DLS runs in the general kernel)

@@ -68,6 +68,7 @@ struct DevScene {
     uint32_t spheres_only;  // no free / mesh triangles: launch the sphere-only kernel
     uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
     uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
+    uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

@@ -80,6 +80,12 @@
 #ifndef RT_SPH_UNROLL
 #define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
 #endif
+#ifndef RT_SPH_NO_L0
+#define RT_SPH_NO_L0 1      // closest_small: no l0 > 0 test (implied by l >= HIT_MIN, see sphere_roots)
+#endif
+#ifndef RT_SPH_SQRT_GUARD
+#define RT_SPH_SQRT_GUARD 1 // sphere roots: the sqrt's tiny-input guard folded into the disc predicate
+#endif
 #ifndef RT_REGEN_MIN
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 #endif
@@ -351,14 +357,25 @@ __device__ __forceinline__ SphDisc sphere_disc(float4 s, float rr, const Ray& r)
     const float consts = dot(oc, oc) - rr;
     return SphDisc{dir, dir * dir - consts};
 }
+// L0 = false drops the l0 > 0 test, for callers that then require !(l < HIT_MIN): with disc,
+// and finite dir and thing2 (scene coordinates below 2^58, DevScene::small_ok), l is finite, and
+// l >= HIT_MIN > 0 implies l0 > 0 (l = l1 > 0 gives l0 >= l1; otherwise l = l0).
+template <bool L0 = true>
 __device__ __forceinline__ bool sphere_roots(SphDisc q, float* l) {
     const bool disc = q.thing2 > 0.0f;
     const float offset = -q.dir;
     // thing2 <= 0 (or NaN) gives a NaN or 0 here, but then disc is false and *l is never used
+#if RT_SPH_SQRT_GUARD
+    // sqrt_nonneg's tiny-input guard as one float compare beside disc (lanes without disc
+    // never use the root, so only disc lanes with thing2 < 2^-80 need sqrtf)
+    float thing = RT_EXACT_FAST ? sqrt_rn(q.thing2) : sqrtf(q.thing2);
+    if (RT_EXACT_FAST && __builtin_expect(disc && q.thing2 < 0x1p-80f, 0)) thing = sqrtf(q.thing2);
+#else
     const float thing = sqrt_nonneg(q.thing2);
+#endif
     const float l0 = offset + thing, l1 = offset - thing;
     *l = l1 > 0.0f ? l1 : l0;  // sphere.rs:95
-    return disc && l0 > 0.0f;
+    return disc && (!L0 || l0 > 0.0f);
 }
 __device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
     return sphere_roots(sphere_disc(s, s.w * s.w, r), l);
@@ -744,7 +761,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
     auto take = [&](const SphDisc& q, uint32_t i) {
         if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) return;  // v false on every lane
         float l;
-        const bool v = sphere_roots(q, &l) & !(l < HIT_MIN);
+        const bool v = sphere_roots<!RT_SPH_NO_L0>(q, &l) & !(l < HIT_MIN);
         any |= v;
         const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
         imin = better ? i : imin;
@@ -784,7 +801,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
         const SphDisc q = sphere_disc(sq, sq.w, r);
         if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) continue;  // v false on every lane
         float l;
-        const bool v = sphere_roots(q, &l) & !(l < HIT_MIN);
+        const bool v = sphere_roots<!RT_SPH_NO_L0>(q, &l) & !(l < HIT_MIN);
         any |= v;
         const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
         imin = better ? i : imin;
@@ -828,7 +845,8 @@ template <bool COUNT, bool GEN>
 __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
 #if RT_SMALL_SCENE
-    if (!GEN && (!COUNT || sc.count_device) && sc.n_spheres <= 32u) return closest_small<COUNT>(sc, k, r, best, st, c);
+    if (!GEN && (!COUNT || sc.count_device) && sc.n_spheres <= 32u && sc.small_ok)
+        return closest_small<COUNT>(sc, k, r, best, st, c);
 #endif
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);

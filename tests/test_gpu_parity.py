@@ -271,6 +271,25 @@ def test_small_scene_closest_sphere_bit_exact(gpu_available, oracle, seed):
     assert np.array_equal(g, o), parity.stats(g, o)
 
 
+def test_sphere_scene_beyond_small_bound(gpu_available, oracle):
+    """A sphere-only scene with a sphere centred at 2^59: the host clears small_ok
+    (runtime.hip), so the sphere-only kernel runs the full KD traversal instead of
+    closest_small, whose root arithmetic assumes coordinates below 2^58.  Still the oracle's
+    image, bit for bit."""
+    from rt_amd import render, scheme
+
+    d = _adversarial_spheres(1)
+    d["scene_members"].append({"!Sphere": {"c": [2.0 ** 59, 1.0, -4.0], "r": 1.0,
+                                           "coloring": {"!Solid": [0.5, 0.5, 0.5]},
+                                           "mat": {"divert_ray": "Diff", "emissive": [1.0, 0.0, 0.0]}}})
+    sc = scheme.load(d)
+    tiles = [(0, 0, 160, 96)]
+    with render.Context(sc) as c:
+        g = c.render(tiles, 0, 3)
+    o = oracle.render(sc, tiles, 0, 3)
+    assert np.array_equal(g, o), parity.stats(g, o)
+
+
 def test_wide_frame_without_pixel_table(gpu_available, oracle):
     """A frame over 65535 pixels wide cannot use the packed (y << 16 | x) pixel table
     (runtime.hip prepare_tiles): the kernels fall back to the binary search over the tiles.
