@@ -25,6 +25,12 @@
 using namespace rtd;
 using namespace rth;
 
+// Radiance buffer cap per queue launch (floats): 16 GiB of 288 GB HBM, so a 1000-spp step of a
+// 1200x600 frame (8.6 GB) is one launch.  Every launch ends in a drain tail (lanes idle while the
+// last paths finish): walled's bench step ran 3.4% faster as one launch than as three of 334 spp
+// (4 GiB cap).  RT_QUEUE_RADIANCE_GIB overrides it; only what a launch needs is allocated.
+static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
+
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -52,6 +58,7 @@ struct rt_ctx {
     uint32_t* gstack = nullptr;   // sphere-only queue kernel's traversal stacks (queue_gstack_bytes)
     size_t gstack_cap = 0;
     int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
+    uint64_t queue_floats = 0;    // RT_QUEUE_RADIANCE_GIB: radiance buffer cap per queue launch
     float last_ms = 0.f;
     std::string err;
 };
@@ -411,6 +418,11 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
     }
+    c->queue_floats = QUEUE_RADIANCE_FLOATS;
+    if (const char* e = std::getenv("RT_QUEUE_RADIANCE_GIB")) {
+        unsigned long v = std::strtoul(e, nullptr, 10);
+        if (v >= 1 && v <= 64) c->queue_floats = (uint64_t)v << 28;
+    }
     return RT_OK;
 }
 
@@ -522,7 +534,6 @@ static int ensure_radiance(rt_ctx* c, uint64_t floats) {
 }
 
 static constexpr uint32_t SAMPLES_PER_LANE_CHUNK = 64;
-static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 30;  // 4 GiB per queue launch (of 288 GB HBM)
 
 // Schedule: the queue (persistent lanes over (pixel, sample) items, tools/variant_bench.py:
 // walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_SCHED=direct or
@@ -570,7 +581,7 @@ static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64
     c->n_launch = 0;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     if (use_queue(c, n_out)) {
-        uint64_t chunk = QUEUE_RADIANCE_FLOATS / (3 * n_out);
+        uint64_t chunk = c->queue_floats / (3 * n_out);
         if (chunk < 1) chunk = 1;
         if (chunk > sample_count) chunk = sample_count ? sample_count : 1;
         int per_cu = 0;  // the queue grid: the resident workgroups of this scene's kernel

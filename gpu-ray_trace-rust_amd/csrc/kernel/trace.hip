@@ -86,6 +86,9 @@
 #ifndef RT_SPH_SQRT_GUARD
 #define RT_SPH_SQRT_GUARD 1 // sphere roots: the sqrt's tiny-input guard folded into the disc predicate
 #endif
+#ifndef RT_DRAW_SQRT
+#define RT_DRAW_SQRT 1      // sqrt of a uniform draw (u, 1 - u) without sqrt_nonneg's tiny-input guard (walled +0.4%, biplane +1.5%)
+#endif
 #ifndef RT_REGEN_MIN
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 #endif
@@ -223,6 +226,14 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
     float s = sqrt_rn(x);
     if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
     return s;
+}
+// sqrtf of a uniform draw u or of 1 - u: both are 0 or >= 2^-24 (rt_rng.h's (x >> 8) * 2^-24,
+// u <= 1 - 2^-24), inside sqrt_rn's exact range, so no tiny-input guard is needed.
+__device__ __forceinline__ float sqrt_draw(float x) {
+#if RT_DRAW_SQRT
+    if (RT_EXACT_FAST) return sqrt_rn(x);
+#endif
+    return sqrt_nonneg(x);
 }
 // nalgebra normalize: a / |a| per component.  div3's guard, specialised: |a_i| < 2^60 follows
 // from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs
@@ -1141,14 +1152,14 @@ __device__ __forceinline__ V3 diff_vec(V3 d, V3 n, float dn, uint32_t* rng) {  /
     V3 yd = normalize(cross(n, xd));
     float u = draw(rng);
     float v = draw(rng);
-    float r = sqrt_nonneg(u);
+    float r = sqrt_draw(u);
     float thet = 2.0f * PI * v;
     float sn, cs;
     (void)rt_sincosf(thet, &sn, &cs);  // glibc's sinf, cosf (rt_libm.h); thet in [0, 2 pi)
     float x = r * cs;
     float y = r * sn;
     // max(1 - u, 0) is 1 - u: u <= 1 - 2^-24
-    return (xd * x + yd * y) + n * sqrt_nonneg(1.0f - u);
+    return (xd * x + yd * y) + n * sqrt_draw(1.0f - u);
 }
 // over_in = n_out / n_in, over_out = n_in / n_out and r0 come precomputed (DevMat): the
 // divisions n1 / n2 and (n1 - n2) / (n1 + n2) of :35,48 depend on the material only.
@@ -1221,7 +1232,7 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint
         float a = sc.lens_r;
         float u = draw(rng);
         float v = draw(rng);
-        float r = sqrt_nonneg(u);
+        float r = sqrt_draw(u);
         float thet = 2.0f * PI * v;
         float sn, cs;
         (void)rt_sincosf(thet, &sn, &cs);  // thet in [0, 2 pi)
