@@ -1608,7 +1608,7 @@ __device__ __forceinline__ void launch_pixel(const LaunchArgs& a, uint32_t o, in
 // by its slowest pixel (mesh scenes, where a sky pixel costs a fraction of an airplane pixel).
 // A wave claims a run of consecutive items per atomic and hands them to its idle lanes in lane
 // order; consecutive items are neighbouring pixels of one sample.  The run length adapts to
-// what is left — about remaining / (RT_QDIV * waves), in multiples of 64, from 64 to RT_QMAX —
+// what is left — about remaining / (RT_QDIV * waves), in multiples of 64, from RT_QMIN(_SPH) to RT_QMAX —
 // so the single counter is hit rarely while most items remain (a cheap scene otherwise
 // saturates it) and balance is fine-grained at the end of the launch.  Each item's radiance goes
 // to radiance[j][o]; fold_kernel then applies the running mean in sample order, so the image is
@@ -1619,10 +1619,22 @@ __device__ __forceinline__ void launch_pixel(const LaunchArgs& a, uint32_t o, in
 #ifndef RT_QMAX
 #define RT_QMAX 1024
 #endif
+// Smallest grab.  The sphere-only kernel's items are cheap (~6 segments of a brute-force loop), so
+// 64-item grabs at the end of a launch put every wave on the one counter about every 7 us and
+// the atomics serialise: 256 ran walled +1.6% (A/B, bit-identical).  Mesh items cost 30x more
+// and need the fine end-of-launch balance: 128 ran biplane -10%.
+#ifndef RT_QMIN
+#define RT_QMIN 64
+#endif
+#ifndef RT_QMIN_SPH
+#define RT_QMIN_SPH 256
+#endif
+template <bool GEN>
 __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_waves) {
+    constexpr uint32_t qmin = GEN ? (uint32_t)RT_QMIN : (uint32_t)RT_QMIN_SPH;
     uint32_t g = remaining / (RT_QDIV * n_waves);
     g &= ~63u;
-    return g < 64u ? 64u : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
+    return g < qmin ? qmin : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
 template <bool GEN, bool DLS = false>
@@ -1654,7 +1666,7 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint32_t grab = grab_size(a.n_items, n_waves);
+    uint32_t grab = grab_size<GEN>(a.n_items, n_waves);
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
@@ -1699,7 +1711,7 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
             if (left < n) {
                 pool = base + (n - left);
                 pool_end = base + grab;
-                grab = grab_size(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+                grab = grab_size<GEN>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
             } else {
                 pool += n;
             }
@@ -1809,7 +1821,7 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
     Ctr<false> c;
     const uint32_t lane = __lane_id();
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint32_t pool = 0, pool_end = 0, grab = grab_size(a.n_items, n_waves);
+    uint32_t pool = 0, pool_end = 0, grab = grab_size<true>(a.n_items, n_waves);
     bool have = false, qdone = false, need = false, tr = false;
     uint32_t slot = 0, node = 0;
     int sp = 0;
@@ -1847,7 +1859,7 @@ __global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
             if (left < n) {
                 pool = base + (n - left);
                 pool_end = base + grab;
-                grab = grab_size(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+                grab = grab_size<true>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
             } else {
                 pool += n;
             }
