@@ -423,6 +423,10 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->queue_floats = (uint64_t)v << 28;
     }
+    if (const char* e = std::getenv("RT_QUEUE_RADIANCE_FLOATS")) {  // tests: force split launches
+        unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v >= 3 && v <= (1ull << 34)) c->queue_floats = (uint64_t)v;
+    }
     return RT_OK;
 }
 

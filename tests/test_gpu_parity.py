@@ -192,6 +192,28 @@ def test_queue_schedule_bit_invariant(gpu_available, monkeypatch, scene_name, sp
     assert np.array_equal(g2, ref2)
 
 
+@pytest.mark.parametrize("scene_name,spp", [("walled", 23), ("biplane", 5)])
+def test_split_queue_launches_bit_invariant(gpu_available, monkeypatch, scene_name, spp):
+    """A radiance cap small enough to split one call into several queue launches (each with
+    its own drain and fold) == one launch, bit for bit (runtime.hip's chunk loop; the bench's
+    1000-spp step is one launch under the default 16 GiB cap)."""
+    from rt_amd import render
+
+    sc = load_scene(scene_name)
+    w, h = sc.info.width, sc.info.height
+    tiles = [(w // 2 - 40, h // 2 - 20, 80, 40), (w - 33, h - 9, 33, 9)]
+    n_pix = 80 * 40 + 33 * 9
+    monkeypatch.delenv("RT_QUEUE_RADIANCE_FLOATS", raising=False)
+    with render.Context(sc) as c1:
+        ref = c1.render(tiles, 0, spp)
+    monkeypatch.setenv("RT_QUEUE_RADIANCE_FLOATS", str(3 * n_pix * 4))  # 4 samples per launch
+    with render.Context(sc) as cs:
+        g = cs.render(tiles, 0, spp)
+        n_split = cs.launch_stats()["n_trace_launches"]
+    assert n_split == -(-spp // 4), n_split
+    assert np.array_equal(g, ref)
+
+
 def _adversarial_spheres(seed: int) -> dict:
     """<= 32 spheres built to make the closest-hit decision hard: duplicates (exact ties),
     concentric shells 1e-4 apart, tangent pairs, tiny spheres, deep overlaps and r = 500 walls
