@@ -1957,7 +1957,10 @@ __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
     // (exact reciprocal + Markstein quotients under their range guard).  The samples' loads are
     // issued FOLD_U at a time ahead of the sequential fold: with few launch pixels (a rank's
     // share at N = 8: 90K threads) one load in flight per thread left the fold latency-bound.
-    constexpr uint32_t FOLD_U = 8;
+#ifndef RT_FOLD_U
+#define RT_FOLD_U 8
+#endif
+    constexpr uint32_t FOLD_U = RT_FOLD_U;
     uint32_t j = 0;
     for (; j + FOLD_U <= a.sample_count; j += FOLD_U) {
         float v[3 * FOLD_U];
