@@ -1,15 +1,21 @@
-// trace.hip — the gfx950 per-pixel path-tracing megakernel.
+// trace.hip — the gfx950 path-tracing kernels behind rt_render (include/rt_abi.h).
 //
-// One lane owns one pixel of a tile for the whole sample range of the launch and keeps the
-// pixel's running mean in registers (draw_scene.rs:81-83), so HBM sees one accumulator read
-// and one write per pixel per launch.  Per sample the lane runs the reference CPU path
+// Product schedule (queue_kernel): a persistent grid of exactly the resident lanes traces
+// (pixel, sample) items until the launch's items run out.  A wave claims a run of consecutive
+// items with one atomic and deals them to its idle lanes; a lane whose path ends writes the
+// sample's radiance to radiance[sample][pixel] and takes the next item, so no lane waits for a
+// slow pixel.  fold_kernel then applies the reference's per-pixel running mean
+// (draw_scene.rs:81-83) in sample order.  Per item the lane runs the reference CPU path
 // (render_to_target_cpu -> radiance, draw_scene.rs:73-84, radiance.rs:20-72) as a loop:
-// camera ray (generate.rs:24-66) -> KD stack traversal (kdtree.rs:58-104) with the leaf test
-// of closest_hit.rs:6-30 -> hit_info / Russian roulette / continue_ray of the hit element
-// (sphere.rs, triangle/generic.rs, distant_cube_map.rs, material/*.rs).
+// camera ray (generate.rs:24-66) -> KD traversal (kdtree.rs:58-104) with the leaf test of
+// closest_hit.rs:6-30 -> hit_info / Russian roulette / continue_ray of the hit element
+// (sphere.rs, triangle/generic.rs, mesh/triangle.rs, distant_cube_map.rs, material/*.rs).
 //
-// The traversal stack lives in LDS (one column per lane), 4 bytes per entry (see closest()):
-// the branch that pushed it; t and the exit distance are recomputed on pop.
+// Two instantiations: GEN = false for sphere-only scenes (walled.yml: spheres and materials in
+// LDS, the exact brute-force bound closest_small), GEN = true for triangles and meshes (the
+// wave tests its lanes' KD leaves cooperatively, stack_search_coop).  trace_kernel (one lane
+// per pixel, running mean in registers) is the direct schedule kept as the tests' second path
+// and, with COUNT, the work counter behind the roofline's algorithmic bytes.
 //
 // Float order matches the oracle operation for operation (compiled with -ffp-contract=off,
 // correctly rounded div/sqrt, and glibc's sinf/cosf/powf restated in include/rt_libm.h); the
@@ -23,72 +29,6 @@
 #include "../../../include/rt_libm.h"
 #include "device_scene.h"
 
-#ifndef RT_LDS_NODES
-#define RT_LDS_NODES 0      // measured: LDS-resident top nodes cost more in waves than they save
-#endif
-#ifndef RT_FASTDIV
-#define RT_FASTDIV 1        // Markstein division by the per-ray reciprocal (bit-identical)
-#endif
-#ifndef RT_SMALL_SCENE
-#define RT_SMALL_SCENE 1    // exact brute-force-bounded traversal for <= 32 spheres (closest_small)
-#endif
-#ifndef RT_DISC_SKIP
-#define RT_DISC_SKIP 1      // closest_small: skip a sphere's roots when no lane's discriminant is positive
-#endif
-#ifndef RT_SMALL_SKIP
-#define RT_SMALL_SKIP 1     // closest_small: no traversal when the closest sphere provably is in the returning leaf
-#endif
-#ifndef RT_LEAF_PMIN
-#define RT_LEAF_PMIN 1      // closest_small: a leaf holding the closest sphere needs no re-test
-#endif
-#ifndef RT_EXACT_FAST
-#define RT_EXACT_FAST 1     // rcp/div via the checked exact FMA identities, sincosf (bit-identical)
-#endif
-#ifndef RT_TRI_BF
-#define RT_TRI_BF 0         // branch-free Moller-Trumbore (same operations, predicates combined): no gain
-#endif
-#ifndef RT_LEAF2
-#define RT_LEAF2 2          // general leaves: refs per step, all their loads issued first (1: plain loop)
-#endif
-#ifndef RT_COOP
-#define RT_COOP 1           // general queue kernel: the wave tests its lanes' leaf refs cooperatively
-#endif
-#ifndef RT_MERGED
-#define RT_MERGED 0         // general queue kernel: one loop of traversal rounds (merged_kernel)
-#endif
-#ifndef RT_DPP_SCAN
-#define RT_DPP_SCAN 1       // wave prefix sums by DPP row shifts / broadcasts (else ds_bpermute)
-#endif
-#ifndef RT_TIMING
-#define RT_TIMING 0         // diagnostic build: wave-clock breakdown (rt_debug_timing), never the product
-#endif
-#ifndef RT_COOP_DELTA
-#define RT_COOP_DELTA 1     // cooperative passes: one shuffle of (off - start) instead of three
-#endif
-#ifndef RT_OWNER_NARROW
-#define RT_OWNER_NARROW 0   // coop passes: search only the owners ending inside the pass (biplane +3%, a380 -1.5%: off)
-#endif
-#ifndef RT_OWNER_SCAN
-#define RT_OWNER_SCAN 0     // cooperative passes: owners by LDS slots + DPP prefix max (+-3%: off; else binary search)
-#endif
-#ifndef RT_SPH_PAIRS
-#define RT_SPH_PAIRS 1      // closest_small: discriminants of two spheres at a time (4: four, no further gain)
-#endif
-#ifndef RT_SPH_PREFETCH
-#define RT_SPH_PREFETCH 0   // closest_small: next sphere's LDS record read ahead of the current test
-#endif
-#ifndef RT_SPH_UNROLL
-#define RT_SPH_UNROLL 1     // unroll of the closest_small brute-force loop (2, 4: no gain measured)
-#endif
-#ifndef RT_SPH_NO_L0
-#define RT_SPH_NO_L0 1      // closest_small: no l0 > 0 test (implied by l >= HIT_MIN, see sphere_roots)
-#endif
-#ifndef RT_SPH_SQRT_GUARD
-#define RT_SPH_SQRT_GUARD 1 // sphere roots: the sqrt's tiny-input guard folded into the disc predicate
-#endif
-#ifndef RT_DRAW_SQRT
-#define RT_DRAW_SQRT 1      // sqrt of a uniform draw (u, 1 - u) without sqrt_nonneg's tiny-input guard (walled +0.4%, biplane +1.5%)
-#endif
 #ifndef RT_REGEN_MIN
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 #endif
@@ -103,31 +43,6 @@
 #endif
 #ifndef RT_LDS_SPHERES
 #define RT_LDS_SPHERES 64   // 1 KiB
-#endif
-#ifndef RT_DIVMK_FCMP
-#define RT_DIVMK_FCMP 0     // div_mk's zero test as a float compare (A/B: no difference; off)
-#endif
-#ifndef RT_GSTACK
-#define RT_GSTACK 1         // sphere-only queue kernel: traversal stack in global memory (used for 0.05 nodes/sample)
-#endif
-#ifndef RT_LDS_MAT
-#define RT_LDS_MAT 1        // sphere-only kernels: sphere materials read from an LDS table
-#endif
-// Cheaper exactness guards (bit-identical either way; A/B on walled in DESIGN.md §8):
-#ifndef RT_NORM_MIN3
-#define RT_NORM_MIN3 1      // normalize: one min3 guard; zero / tiny components take the IEEE division
-#endif
-#ifndef RT_G2_NORM
-#define RT_G2_NORM 0        // normalize: copysign instead of div_mk's zero test (-2.5%: off)
-#endif
-#ifndef RT_G2_RCP
-#define RT_G2_RCP 1         // ray_axes / Moller-Trumbore: one-compare guard for reciprocals of |b| >= EPS
-#endif
-#ifndef RT_G2_IRL
-#define RT_G2_IRL 1         // in_return_leaf: no zero test on quotients that are only compared
-#endif
-#ifndef RT_NORM_GUARD
-#define RT_NORM_GUARD 1     // normalize: the Markstein range guard by float compares (see below)
 #endif
 
 namespace rtd {
@@ -174,11 +89,7 @@ __device__ __forceinline__ float rcp_exact(float b) {
 __device__ __forceinline__ float div_mk(float a, float b, float r) {
     const float q0 = a * r;
     const float q = fmaf(fmaf(-q0, b, a), r, q0);
-#if RT_DIVMK_FCMP
-    return a == 0.0f ? a : q;  // +-0 keeps its sign (one float compare; NaN is not 0)
-#else
     return (__float_as_uint(a) << 1) == 0u ? a : q;
-#endif
 }
 // The Markstein quotient without div_mk's zero test: exact for nonzero a in range; a = +-0
 // gives +0 (callers that need the sign of a zero restore it, or only compare the result).
@@ -189,21 +100,18 @@ __device__ __forceinline__ float div_mk_nz(float a, float b, float r) {
 // 1.0f / b for a b the caller knows is not below 2^-60 in magnitude (or whose reciprocal it
 // discards otherwise): one compare guards the top of the exact range.
 __device__ __forceinline__ float recip_big(float b) {
-    if (!RT_EXACT_FAST) return 1.0f / b;
     float r = rcp_exact(b);
     if (__builtin_expect(!(fabsf(b) < 0x1p60f), 0)) r = 1.0f / b;
     return r;
 }
 // 1.0f / b, bit for bit
 __device__ __forceinline__ float recip(float b) {
-    if (!RT_EXACT_FAST) return 1.0f / b;
     float r = rcp_exact(b);
     if (__builtin_expect(!mk_range(b), 0)) r = 1.0f / b;
     return r;
 }
 // (a.x / b, a.y / b, a.z / b), bit for bit
 __device__ __forceinline__ V3 div3(V3 a, float b) {
-    if (!RT_EXACT_FAST) return a / b;
     const float r = rcp_exact(b);
     V3 q = mk(div_mk(a.x, b, r), div_mk(a.y, b, r), div_mk(a.z, b, r));
     if (__builtin_expect(!(mk_range(b) && mk_num(a.x) && mk_num(a.y) && mk_num(a.z)), 0)) q = a / b;
@@ -222,7 +130,6 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 // and is >= 0x7fffffff for -0, so one compare sends exactly (0, 2^-80) to sqrtf — a divergent
 // branch no lane normally takes.  (A NaN x gives a NaN either way.)
 __device__ __forceinline__ float sqrt_nonneg(float x) {
-    if (!RT_EXACT_FAST) return sqrtf(x);
     float s = sqrt_rn(x);
     if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
     return s;
@@ -230,22 +137,14 @@ __device__ __forceinline__ float sqrt_nonneg(float x) {
 // sqrtf of a uniform draw u or of 1 - u: both are 0 or >= 2^-24 (rt_rng.h's (x >> 8) * 2^-24,
 // u <= 1 - 2^-24), inside sqrt_rn's exact range, so no tiny-input guard is needed.
 __device__ __forceinline__ float sqrt_draw(float x) {
-#if RT_DRAW_SQRT
-    if (RT_EXACT_FAST) return sqrt_rn(x);
-#endif
-    return sqrt_nonneg(x);
+    return sqrt_rn(x);
 }
 // nalgebra normalize: a / |a| per component.  div3's guard, specialised: |a_i| < 2^60 follows
-// from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs
-// "zero or |a_i| >= 2^-60" — one compare with a free abs modifier and one equality.  A NaN
-// numerator makes |a| NaN, which fails mk_range.
-__device__ __forceinline__ bool tiny_ok(float x) { return !(fabsf(x) < 0x1p-60f) || x == 0.0f; }
+// from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs to be
+// nonzero with |a_i| >= 2^-60.  A NaN numerator makes |a| NaN, which fails mk_range.
 __device__ __forceinline__ V3 normalize(V3 a) {
     float n = sqrt_nonneg(dot(a, a));
-#if RT_NORM_GUARD
-    if (!RT_EXACT_FAST) return a / n;
     const float r = rcp_exact(n);
-#if RT_NORM_MIN3
     // Common case: every |a_i| >= 2^-60 (one v_min3 and one compare), so no numerator is zero
     // and div_mk's zero test is not needed either.  A zero or tiny component, or n out of range,
     // takes the IEEE division (a divergent branch that lanes rarely take).
@@ -253,20 +152,6 @@ __device__ __forceinline__ V3 normalize(V3 a) {
     const float amin = fminf(fminf(fabsf(a.x), fabsf(a.y)), fabsf(a.z));
     if (__builtin_expect(!(mk_range(n) && amin >= 0x1p-60f), 0)) q = a / n;
     return q;
-#elif RT_G2_NORM
-    // n > 0, so a_i / n has a_i's sign: the Markstein quotient is exact in magnitude (also for
-    // a_i = -0, where it yields +0), and copysign restores the sign — one v_bfi instead of
-    // div_mk's zero test and select.
-    V3 q = mk(copysignf(div_mk_nz(a.x, n, r), a.x), copysignf(div_mk_nz(a.y, n, r), a.y),
-              copysignf(div_mk_nz(a.z, n, r), a.z));
-#else
-    V3 q = mk(div_mk(a.x, n, r), div_mk(a.y, n, r), div_mk(a.z, n, r));
-#endif
-    if (__builtin_expect(!(mk_range(n) && tiny_ok(a.x) && tiny_ok(a.y) && tiny_ok(a.z)), 0)) q = a / n;
-    return q;
-#else
-    return div3(a, n);
-#endif
 }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -301,56 +186,31 @@ struct Ctr {
     uint32_t nodes = 0, leaf_refs = 0, sph = 0, tri = 0, segments = 0, hits = 0, mesh_hits = 0;
 };
 
-// Workgroup-shared copies (LDS) of the hottest scene data: the first `n_nodes` nodes of the
-// breadth-first node array (the top levels of the tree, visited by every descent) and the
-// first `n_sph` spheres.  Indices past them read HBM (through L2 / MALL).
+// Workgroup-shared copies (LDS) of the sphere-only kernel's scene data: every sphere, its
+// {c, fl(r * r)} and its material (the host launches that kernel only when they all fit).
 // The LDS copies are file-scope __shared__ arrays referenced directly, so loads from them are
 // ds_read (a pointer that may be LDS or global would become a slower FLAT load).
-#if RT_LDS_NODES > 0
-__shared__ uint2 g_lds_nodes[RT_LDS_NODES];
-#endif
-#if RT_LDS_SPHERES > 0
 __shared__ float4 g_lds_sph[RT_LDS_SPHERES];
 __shared__ float4 g_lds_csq[RT_LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
-#if RT_LDS_MAT
 __shared__ DevMat g_lds_mat[RT_LDS_SPHERES];
-#endif
-#endif
-struct Cache {
-    uint32_t n_nodes;  // nodes [0, n_nodes) are in g_lds_nodes
-    uint32_t n_sph;    // spheres [0, n_sph) are in g_lds_sph
-};
-__device__ __forceinline__ uint2 fetch_node(const DevScene& sc, const Cache& k, uint32_t i) {
-#if RT_LDS_NODES > 0
-    if (i < k.n_nodes) return g_lds_nodes[i];
-#endif
-    (void)k;
-    return sc.nodes[i];
-}
-// GEN == false (sphere-only kernel, launched only when every sphere fits the LDS table):
-// spheres come from LDS only.  The general kernel reads them from global memory.
+__device__ __forceinline__ uint2 fetch_node(const DevScene& sc, uint32_t i) { return sc.nodes[i]; }
+// GEN == false (sphere-only kernel): spheres come from LDS.  The general kernel reads them from
+// global memory.
 template <bool GEN>
-__device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, const Cache& k, uint32_t i) {
-    (void)k;
-#if RT_LDS_SPHERES > 0
+__device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, uint32_t i) {
     if (!GEN) return g_lds_sph[i];
-#endif
     return sc.sph[i];
 }
 
-#if RT_LDS_SPHERES > 0
-__device__ __forceinline__ void fill_lds_spheres(const DevScene& sc, Cache& k) {
-    k.n_sph = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
-    for (uint32_t i = threadIdx.x; i < k.n_sph; i += BLOCK) {
+__device__ __forceinline__ void fill_lds_spheres(const DevScene& sc) {
+    const uint32_t n = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
         const float4 v = sc.sph[i];
         g_lds_sph[i] = v;
         g_lds_csq[i] = make_float4(v.x, v.y, v.z, v.w * v.w);
-#if RT_LDS_MAT
         g_lds_mat[i] = sc.sph_mat[i];
-#endif
     }
 }
-#endif
 
 // ---------------------------------------------------------------- primitives
 // Sphere::intersect (sphere.rs:83-105) in two steps: the discriminant (sphere_disc, with
@@ -376,14 +236,10 @@ __device__ __forceinline__ bool sphere_roots(SphDisc q, float* l) {
     const bool disc = q.thing2 > 0.0f;
     const float offset = -q.dir;
     // thing2 <= 0 (or NaN) gives a NaN or 0 here, but then disc is false and *l is never used
-#if RT_SPH_SQRT_GUARD
     // sqrt_nonneg's tiny-input guard as one float compare beside disc (lanes without disc
     // never use the root, so only disc lanes with thing2 < 2^-80 need sqrtf)
-    float thing = RT_EXACT_FAST ? sqrt_rn(q.thing2) : sqrtf(q.thing2);
-    if (RT_EXACT_FAST && __builtin_expect(disc && q.thing2 < 0x1p-80f, 0)) thing = sqrtf(q.thing2);
-#else
-    const float thing = sqrt_nonneg(q.thing2);
-#endif
+    float thing = sqrt_rn(q.thing2);
+    if (__builtin_expect(disc && q.thing2 < 0x1p-80f, 0)) thing = sqrtf(q.thing2);
     const float l0 = offset + thing, l1 = offset - thing;
     *l = l1 > 0.0f ? l1 : l0;  // sphere.rs:95
     return disc && (!L0 || l0 > 0.0f);
@@ -400,11 +256,7 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
     V3 ray_x_e2 = cross(r.d, e2);
     float det = dot(e1, ray_x_e2);
     if (fabsf(det) < EPS) return false;
-#if RT_G2_RCP
     float inv_det = recip_big(det);  // |det| >= EPS here
-#else
-    float inv_det = recip(det);
-#endif
     V3 rhs = r.o - v0;
     float u = inv_det * dot(rhs, ray_x_e2);
     if (u < 0.0f || u > 1.0f) return false;
@@ -419,30 +271,6 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float
     return true;
 }
 
-// The same test without early exits: every quantity is computed with the reference's operations
-// and order, and the four rejections are combined into one predicate (NaN compares exactly as
-// the early exits do).  inv_det is exact for |det| in [EPS, 2^60) (rcp_exact); a rejected det's
-// reciprocal is never used.
-__device__ __forceinline__ bool tri_hit_bf(V3 v0, V3 v1, V3 v2, const Ray& r, float* l, float* bu,
-                                           float* bv) {
-    const V3 e1 = v1 - v0;
-    const V3 e2 = v2 - v0;
-    const V3 ray_x_e2 = cross(r.d, e2);
-    const float det = dot(e1, ray_x_e2);
-    float inv_det = RT_EXACT_FAST ? rcp_exact(det) : 1.0f / det;
-    if (RT_EXACT_FAST && __builtin_expect(fabsf(det) >= 0x1p60f, 0)) inv_det = 1.0f / det;
-    const V3 rhs = r.o - v0;
-    const float u = inv_det * dot(rhs, ray_x_e2);
-    const V3 rhs_x_e1 = cross(rhs, e1);
-    const float v = inv_det * dot(r.d, rhs_x_e1);
-    const float t = inv_det * dot(e2, rhs_x_e1);
-    *l = t;
-    *bu = u;
-    *bv = v;
-    return !(fabsf(det) < EPS) & !(u < 0.0f || u > 1.0f) & !(v < 0.0f || (u + v) > 1.0f) & !(t < EPS);
-}
-
-// Aabb::get_entry_exit (aabb.rs:22-62)
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
 // hits not shorter than 20*EPS.
 // Device data of a leaf ref: a sphere's float4 {c, r} or a triangle's three vertices.
@@ -475,11 +303,7 @@ __device__ __forceinline__ void leaf_step(const LeafSlot& sl, const Ray& r, Hit*
         h = sphere_hit(a0, r, &l);
     } else {
         if (COUNT) c.tri++;
-#if RT_TRI_BF
-        h = tri_hit_bf(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
-#else
         h = tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
-#endif
     }
     const bool above = !raylen_less(l, HIT_MIN);  // RayLen order: NaN sorts above everything
     const bool closer = raylen_less(l, best->l);
@@ -492,10 +316,10 @@ __device__ __forceinline__ void leaf_step(const LeafSlot& sl, const Ray& r, Hit*
 }
 
 template <bool COUNT, bool GEN, bool SMALL = false>
-__device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k, uint32_t off,
+__device__ __forceinline__ bool leaf_closest(const DevScene& sc, uint32_t off,
                                              uint32_t cnt, const Ray& r, Hit* best, Ctr<COUNT>& c,
                                              uint32_t imin = 0, float lmin = 0.f) {
-    if (SMALL && RT_LEAF_PMIN) {
+    if (SMALL) {
         // If the leaf holds the globally closest sphere, that sphere is its candidate: no other
         // leaf sphere is closer, and on a tie the lowest renderable index wins both globally and
         // in leaf order.  Only otherwise are the leaf's spheres re-tested.
@@ -509,33 +333,22 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
         }
     }
     bool found = false;
-#if RT_LEAF2
     if (GEN && !SMALL) {
-        // RT_LEAF2 refs per step: every ref and every primitive's data of the step is loaded
-        // before any is tested, so a lane keeps RT_LEAF2 dependent load chains in flight.  A
-        // sphere reads its float4 and the two padding float4s after it (the array is padded);
-        // steps past the leaf's end re-read its last ref and skip the test.
-        constexpr uint32_t N = RT_LEAF2 > 1 ? RT_LEAF2 : 1;
-        static_assert(N <= 4, "RT_LEAF2 <= 4");
-        for (uint32_t j = 0; j < cnt; j += N) {
-            const uint32_t last = cnt - 1;
-            LeafSlot s0, s1, s2, s3;
+        // Two refs per step: both refs and both primitives' data are loaded before either is
+        // tested, so a lane keeps two dependent load chains in flight.  A sphere reads its float4
+        // and the two padding float4s after it (the array is padded); a step past the leaf's end
+        // re-reads its last ref and skips the test.
+        for (uint32_t j = 0; j < cnt; j += 2) {
+            LeafSlot s0, s1;
             s0.ref = sc.refs[off + j];
-            if constexpr (N > 1) s1.ref = sc.refs[off + (j + 1 < cnt ? j + 1 : last)];
-            if constexpr (N > 2) s2.ref = sc.refs[off + (j + 2 < cnt ? j + 2 : last)];
-            if constexpr (N > 3) s3.ref = sc.refs[off + (j + 3 < cnt ? j + 3 : last)];
+            s1.ref = sc.refs[off + (j + 1 < cnt ? j + 1 : cnt - 1)];
             s0.load(sc);
-            if constexpr (N > 1) s1.load(sc);
-            if constexpr (N > 2) s2.load(sc);
-            if constexpr (N > 3) s3.load(sc);
+            s1.load(sc);
             leaf_step<COUNT>(s0, r, best, found, c);
-            if constexpr (N > 1) if (j + 1 < cnt) leaf_step<COUNT>(s1, r, best, found, c);
-            if constexpr (N > 2) if (j + 2 < cnt) leaf_step<COUNT>(s2, r, best, found, c);
-            if constexpr (N > 3) if (j + 3 < cnt) leaf_step<COUNT>(s3, r, best, found, c);
+            if (j + 1 < cnt) leaf_step<COUNT>(s1, r, best, found, c);
         }
         return found;
     }
-#endif
     for (uint32_t j = 0; j < cnt; ++j) {
         uint32_t ref = sc.refs[off + j];
         uint32_t kind = ref >> REF_KIND_SHIFT, idx = ref & REF_INDEX_MASK;
@@ -543,7 +356,7 @@ __device__ __forceinline__ bool leaf_closest(const DevScene& sc, const Cache& k,
         bool h;
         if (!GEN || kind == K_SPHERE) {
             if (COUNT) c.sph++;
-            h = sphere_hit(fetch_sphere<GEN>(sc, k, idx), r, &l);
+            h = sphere_hit(fetch_sphere<GEN>(sc, idx), r, &l);
         } else {
             if (COUNT) c.tri++;
             const float4* v = sc.prim4 + 3 * (size_t)idx;
@@ -574,15 +387,9 @@ __device__ __forceinline__ RayAx ray_axes(const Ray& r) {
     x.dx = clamp_eps(r.d.x);
     x.dy = clamp_eps(r.d.y);
     x.dz = clamp_eps(r.d.z);
-#if RT_G2_RCP
     x.rx = recip_big(x.dx);  // clamped: |d| >= EPS (or NaN, which recip_big sends to 1 / d)
     x.ry = recip_big(x.dy);
     x.rz = recip_big(x.dz);
-#else
-    x.rx = recip(x.dx);
-    x.ry = recip(x.dy);
-    x.rz = recip(x.dz);
-#endif
     return x;
 }
 // Branch-free pick by axis a in {0,1,2}.
@@ -663,14 +470,14 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
 // stack top when nothing is pushed; a branch at depth D has sp <= D < stack_depth) and sp only
 // advances on a push, so the three reference cases (near / far / push both) are selects.
 template <bool COUNT, bool GEN, bool FAST, bool SMALL = false>
-__device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
+__device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, const RayAx& ax,
                                              float root_entry, float root_exit, Hit* best, uint32_t* st,
                                              Ctr<COUNT>& c, uint32_t imin = 0, float lmin = 0.f) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0;
     int sp = 0;
     for (;;) {
-        uint2 nd = fetch_node(sc, k, node);
+        uint2 nd = fetch_node(sc, node);
         while ((nd.y & 3u) != RT_KD_LEAF) {
             if (COUNT) c.nodes++;
             float d;
@@ -684,21 +491,21 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Cache& k,
             top_t = push ? t : top_t;
             exit_t = push ? t : exit_t;
             node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
-            nd = fetch_node(sc, k, node);
+            nd = fetch_node(sc, node);
         }
         if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-        if (leaf_closest<COUNT, GEN, SMALL>(sc, k, nd.y >> 2, nd.x, r, best, c, imin, lmin) &&
+        if (leaf_closest<COUNT, GEN, SMALL>(sc, nd.y >> 2, nd.x, r, best, c, imin, lmin) &&
             best->l <= exit_t + EPS)
             return true;
         if (sp == 0) return false;
         --sp;
-        const uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
+        const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
         float d;
         (void)split_t<FAST>(pn, ax, r, &d);
         node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);  // the far child
         entry = top_t;
         if (sp) {
-            top_t = split_t<FAST>(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
+            top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
             exit_t = top_t;
         } else {
             exit_t = root_exit;
@@ -731,12 +538,8 @@ __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const Ray
         const float d = a == 0 ? ax.dx : (a == 1 ? ax.dy : ax.dz);
         const float rc = a == 0 ? ax.rx : (a == 1 ? ax.ry : ax.rz);
         const float nlo = (c - s.w) - o, nhi = (c + s.w) - o;
-#if RT_G2_IRL
         // only compared below: the sign of a zero quotient does not matter
         const float tlo = div_mk_nz(nlo, d, rc), thi = div_mk_nz(nhi, d, rc);
-#else
-        const float tlo = div_mk(nlo, d, rc), thi = div_mk(nhi, d, rc);
-#endif
         const float tn = d > 0.0f ? tlo : thi, tf = d > 0.0f ? thi : tlo;
         ok &= mk_num(nlo) && mk_num(nhi);
         ok &= (tn <= e) && (tf > ls);
@@ -757,39 +560,24 @@ __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const Ray
 // need no descent at all (in_return_leaf).  The instrumented kernel counts the reference's work with the plain traversal and the device's
 // work (count_device) through this function.
 template <bool COUNT>
-__device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
+__device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, Hit* best,
                                               uint32_t* st, Ctr<COUNT>& c) {
     uint32_t imin = 0;
     bool any = false;
     float ls = __builtin_inff();
     if (COUNT) c.sph += sc.n_spheres;
-#if RT_SPH_PREFETCH
-    float4 sq_next = g_lds_csq[0];
-#endif
-#if RT_SPH_PAIRS
     // Spheres in pairs: the two discriminants are independent, so their arithmetic interleaves
     // (the per-sphere skip branch keeps the compiler from overlapping consecutive iterations).
     auto take = [&](const SphDisc& q, uint32_t i) {
-        if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) return;  // v false on every lane
+        if (__builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) return;  // v false on every lane
         float l;
-        const bool v = sphere_roots<!RT_SPH_NO_L0>(q, &l) & !(l < HIT_MIN);
+        const bool v = sphere_roots<false>(q, &l) & !(l < HIT_MIN);
         any |= v;
         const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
         imin = better ? i : imin;
         ls = better ? l : ls;
     };
     uint32_t i = 0;
-#if RT_SPH_PAIRS >= 4
-    for (; i + 3 < sc.n_spheres; i += 4) {
-        const float4 sa = g_lds_csq[i], sb = g_lds_csq[i + 1], sc2 = g_lds_csq[i + 2], sd = g_lds_csq[i + 3];
-        const SphDisc qa = sphere_disc(sa, sa.w, r), qb = sphere_disc(sb, sb.w, r);
-        const SphDisc qc = sphere_disc(sc2, sc2.w, r), qd = sphere_disc(sd, sd.w, r);
-        take(qa, i);
-        take(qb, i + 1);
-        take(qc, i + 2);
-        take(qd, i + 3);
-    }
-#endif
     for (; i + 1 < sc.n_spheres; i += 2) {
         const float4 sa = g_lds_csq[i], sb = g_lds_csq[i + 1];
         const SphDisc qa = sphere_disc(sa, sa.w, r), qb = sphere_disc(sb, sb.w, r);
@@ -800,48 +588,25 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
         const float4 sa = g_lds_csq[i];
         take(sphere_disc(sa, sa.w, r), i);
     }
-#else
-#pragma unroll RT_SPH_UNROLL
-    for (uint32_t i = 0; i < sc.n_spheres; ++i) {
-#if RT_SPH_PREFETCH
-        const float4 sq = sq_next;
-        sq_next = g_lds_csq[i + 1];  // the table has RT_LDS_SPHERES > 32 entries
-#else
-        const float4 sq = g_lds_csq[i];
-#endif
-        const SphDisc q = sphere_disc(sq, sq.w, r);
-        if (RT_DISC_SKIP && __builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) continue;  // v false on every lane
-        float l;
-        const bool v = sphere_roots<!RT_SPH_NO_L0>(q, &l) & !(l < HIT_MIN);
-        any |= v;
-        const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
-        imin = better ? i : imin;
-        ls = better ? l : ls;
-    }
-#endif
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (any && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
         // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
         const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
-#if RT_SMALL_SKIP
         // (COUNT here means the device-work count: closest_small never runs for the reference's)
-        if (root_entry <= ls && ls <= root_exit + EPS && in_return_leaf(fetch_sphere<false>(sc, k, imin), r, ax, e, ls)) {
+        if (root_entry <= ls && ls <= root_exit + EPS && in_return_leaf(fetch_sphere<false>(sc, imin), r, ax, e, ls)) {
             best->ref = (K_SPHERE << REF_KIND_SHIFT) | imin;
             best->l = ls;
             best->bu = best->bv = 0.f;
             return true;
         }
-#endif
         const float entry = fmaxf(root_entry, e);
         bool found;
-#if RT_FASTDIV
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, false, true, true>(sc, k, r, ax, entry, root_exit, best, st, c, imin, ls);
+            found = stack_search<COUNT, false, true, true>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
         else
-#endif
-            found = stack_search<COUNT, false, false, true>(sc, k, r, ax, entry, root_exit, best, st, c, imin, ls);
+            found = stack_search<COUNT, false, false, true>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
         if (found) return true;
     }
     if (sc.has_cube) {
@@ -853,23 +618,19 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Cache& k
 }
 
 template <bool COUNT, bool GEN>
-__device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
+__device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
-#if RT_SMALL_SCENE
     if (!GEN && (!COUNT || sc.count_device) && sc.n_spheres <= 32u && sc.small_ok)
-        return closest_small<COUNT>(sc, k, r, best, st, c);
-#endif
+        return closest_small<COUNT>(sc, r, best, st, c);
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
         bool found;
-#if RT_FASTDIV
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, GEN, true>(sc, k, r, ax, root_entry, root_exit, best, st, c);
+            found = stack_search<COUNT, GEN, true>(sc, r, ax, root_entry, root_exit, best, st, c);
         else
-#endif
-            found = stack_search<COUNT, GEN, false>(sc, k, r, ax, root_entry, root_exit, best, st, c);
+            found = stack_search<COUNT, GEN, false>(sc, r, ax, root_entry, root_exit, best, st, c);
         if (found) return true;
     }
     // unconditional renderables: every cube map hits at +inf, the first one wins
@@ -891,19 +652,9 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Cache& k, cons
 // (bits(l) << 32 | position in the leaf): positive floats order like their bit patterns, so this
 // is the first strict minimum in leaf order (closest_hit.rs:25), exactly; NaN lengths never
 // win (see leaf_closest).  The owner then re-tests the winning ref for its barycentrics.
-#if RT_COOP
 __shared__ unsigned long long g_coop_key[BLOCK];
 __shared__ uint32_t g_coop_slot[BLOCK];
-#endif
 
-#if RT_TIMING
-// Diagnostic build only (-DRT_TIMING=1): wave-clock breakdown of the queue kernels.
-// General kernel: [0] descent + pop cycles, [1] cooperative pass cycles, [2] traversal rounds,
-// [3] passes, [5] closest_coop calls.  Sphere-only kernel: [0] item grab + path start,
-// [1] closest, [2] shade, [3] loop iterations.  [4] queue-kernel cycles (summed over waves).
-__device__ unsigned long long g_rt_timing[8];
-#define RT_CLOCK() __builtin_amdgcn_s_memtime()
-#endif
 
 // Inclusive prefix maximum over the 64 lanes (the DPP pattern of wave_incl_scan with max).
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
@@ -921,7 +672,6 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
 // r's total to row r+1 for rows 1 and 3, row_bcast:31 adds rows 0-1's total to rows 2-3.  No
 // LDS, no per-lane address registers (the ds_bpermute form kept six of them live).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
-#if RT_DPP_SCAN
     (void)lane;
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
@@ -930,14 +680,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
     return v;
-#else
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(v, d);
-        v += lane >= d ? u : 0u;
-    }
-    return v;
-#endif
 }
 
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
@@ -945,55 +687,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 // leaf's refs are contiguous, so the index orders like the position in the leaf.
 __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
                                                         uint32_t cnt, uint32_t lane) {
-#if RT_COOP
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
     __hip_atomic_store(&g_coop_key[threadIdx.x], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t w = base + lane;
-#if RT_OWNER_SCAN
-        // The owner of item w is the first lane whose inclusive end exceeds w.  The pass's first
-        // item's owner is the count of lanes ending at or before it (one ballot); every other
-        // owner starting inside the pass marks its start slot; a prefix maximum over the slots
-                // gives each lane its owner (+1).  Owners with items have distinct starts: no collision.
-        // (relaxed wavefront-scope atomics: lanes talk through LDS, and a plain access would let
-        // the compiler forward a lane's own store to its read, missing the other lanes' writes)
-        const uint32_t first = (uint32_t)__popcll(__ballot(incl <= base));
-        __hip_atomic_store(&g_coop_slot[threadIdx.x], lane == 0 ? first + 1u : 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WAVEFRONT);
-        const uint32_t start = incl - cnt;
-        if (cnt && start > base && start < base + 64u)
-            __hip_atomic_store(&g_coop_slot[wbase + (start - base)], lane + 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WAVEFRONT);
-        const uint32_t owner =
-            wave_incl_max(__hip_atomic_load(&g_coop_slot[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) - 1u;
-#elif RT_OWNER_NARROW
-        // The owner of item w is the number of lanes whose inclusive end is <= w.  Lanes ending at
-        // or before the pass start are counted by one ballot; only the n lanes that end inside
-        // the pass remain to be searched, in ceil(log2(n + 1)) shuffle steps (wave-uniform) instead
-        // of 6 — lanes past them end after the pass, so the search never runs beyond them.
-        uint32_t owner = (uint32_t)__popcll(__ballot(incl <= base));
-        const uint32_t n_in = (uint32_t)__popcll(__ballot(incl > base && incl < base + 64u));
-        for (uint32_t step = n_in ? 1u << (31 - __builtin_clz(n_in)) : 0u; step; step >>= 1) {
-            const uint32_t e = __shfl(incl, min(owner + step - 1, 63u));  // lane 63 ends at total > w
-            owner += e <= w ? step : 0u;
-        }
-#else
         uint32_t owner = 0;  // lanes whose inclusive end is <= w
 #pragma unroll
         for (uint32_t step = 32; step; step >>= 1) {
             const uint32_t e = __shfl(incl, owner + step - 1);
             owner += e <= w ? step : 0u;
         }
-#endif
-#if RT_COOP_DELTA
         // item w of the owner's leaf is sc.refs[w + (off - start)] of the owner: one shuffle
         const uint32_t idx = w + __shfl(off - (incl - cnt), owner);
-#else
-        const uint32_t o_end = __shfl(incl, owner), o_cnt = __shfl(cnt, owner), o_off = __shfl(off, owner);
-        const uint32_t idx = o_off + (w - (o_end - o_cnt));
-#endif
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
@@ -1009,16 +716,12 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
         }
     }
     return __hip_atomic_load(&g_coop_key[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#else
-    (void)sc; (void)r; (void)off; (void)cnt; (void)lane;
-    return ~0ull;
-#endif
 }
 
 // stack_search with cooperative leaves: the same per-lane traversal (kdtree.rs:66-104); lanes
 // whose search has ended (or that had no ray) keep looping as helpers until the wave is done.
 template <bool FAST>
-__device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
+__device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
                                                   uint32_t* st) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
@@ -1026,17 +729,10 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
     int sp = 0;
     bool done = !active, found = false;
     const uint32_t lane = __lane_id();
-#if RT_TIMING
-    unsigned long long t_desc = 0, t_pass = 0, rounds = 0, passes = 0;
-#endif
     while (__ballot(!done) != 0) {
-#if RT_TIMING
-        const unsigned long long T0 = RT_CLOCK();
-        ++rounds;
-#endif
         uint32_t off = 0, cnt = 0;
         if (!done) {
-            uint2 nd = fetch_node(sc, k, node);
+            uint2 nd = fetch_node(sc, node);
             while ((nd.y & 3u) != RT_KD_LEAF) {
                 float d;
                 const float t = split_t<FAST>(nd, ax, r, &d);
@@ -1049,21 +745,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
                 top_t = push ? t : top_t;
                 exit_t = push ? t : exit_t;
                 node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
-                nd = fetch_node(sc, k, node);
+                nd = fetch_node(sc, node);
             }
             off = nd.y >> 2;
             cnt = nd.x;
         }
-#if RT_TIMING
-        passes += (__shfl(wave_incl_scan(cnt, lane), 63) + 63) / 64;
-        const unsigned long long T1 = RT_CLOCK();
-#endif
         const unsigned long long key = coop_leaf(sc, r, off, cnt, lane);
-#if RT_TIMING
-        const unsigned long long T2 = RT_CLOCK();
-        t_pass += T2 - T1;
-        t_desc += T1 - T0;
-#endif
         if (!done) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
@@ -1085,50 +772,36 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Cach
                 done = true;
             } else {
                 --sp;
-                const uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
+                const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
                 float d;
                 (void)split_t<FAST>(pn, ax, r, &d);
                 node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
                 entry = top_t;
                 if (sp) {
-                    top_t = split_t<FAST>(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
+                    top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
                     exit_t = top_t;
                 } else {
                     exit_t = root_exit;
                 }
             }
         }
-#if RT_TIMING
-        t_desc += RT_CLOCK() - T2;
-#endif
     }
-#if RT_TIMING
-    if (lane == 0) {
-        atomicAdd(&g_rt_timing[0], t_desc);
-        atomicAdd(&g_rt_timing[1], t_pass);
-        atomicAdd(&g_rt_timing[2], rounds);
-        atomicAdd(&g_rt_timing[3], passes);
-        atomicAdd(&g_rt_timing[5], 1ull);
-    }
-#endif
     return found;
 }
 
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
-__device__ __forceinline__ bool closest_coop(const DevScene& sc, const Cache& k, const Ray& r, Hit* best,
+__device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
                                              uint32_t* st, bool active) {
     float root_entry = 0.f, root_exit = 0.f;
     const RayAx ax = ray_axes(r);
     const bool in = active && sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit);
     bool found;
-#if RT_FASTDIV
     const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
     if (__builtin_expect(__ballot(!fast) == 0, 1))
-        found = stack_search_coop<true>(sc, k, r, ax, in, root_entry, root_exit, best, st);
+        found = stack_search_coop<true>(sc, r, ax, in, root_entry, root_exit, best, st);
     else
-#endif
-        found = stack_search_coop<false>(sc, k, r, ax, in, root_entry, root_exit, best, st);
+        found = stack_search_coop<false>(sc, r, ax, in, root_entry, root_exit, best, st);
     if (found) return true;
     if (active && sc.has_cube) {
         best->ref = REF_CUBE;
@@ -1139,7 +812,7 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Cache& k,
 }
 
 // ---------------------------------------------------------------- materials (interaction.rs)
-__device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rng); }
+__device__ __forceinline__ float draw(rt_rng_state* rng) { return rt_rng_next_f32(rng); }
 
 // Every continued direction of interaction.rs ends in a normalize, and so does the camera ray.
 // The *_vec functions (and the mirror direction, computed inline) return the vector before it, and segment() normalizes once at its start:
@@ -1147,7 +820,7 @@ __device__ __forceinline__ float draw(uint32_t* rng) { return rt_rng_next_f32(rn
 // normalize at full width instead of one per branch at partial width.  Each lane still
 // normalizes exactly the vector the reference does.
 // dn = dot(d, n), shared by the callers' branches
-__device__ __forceinline__ V3 diff_vec(V3 d, V3 n, float dn, uint32_t* rng) {  // :11-27
+__device__ __forceinline__ V3 diff_vec(V3 d, V3 n, float dn, rt_rng_state* rng) {  // :11-27
     V3 xd = normalize(d - n * dn);
     V3 yd = normalize(cross(n, xd));
     float u = draw(rng);
@@ -1168,7 +841,7 @@ __device__ __forceinline__ V3 diff_vec(V3 d, V3 n, float dn, uint32_t* rng) {  /
 // of :6-9, come from the caller; the mirror about -n is the same vector bit for bit (each
 // negation is exact).
 __device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float dn, V3 refl, float over_in, float over_out,
-                                          float r0, float* p, uint32_t* rng) {  // :29-59
+                                          float r0, float* p, rt_rng_state* rng) {  // :29-59
     float c_ = dn;
     bool into = c_ < 0.0f;
     float c1 = into ? -c_ : c_;
@@ -1222,7 +895,7 @@ __device__ __forceinline__ V3 cube_emissive(const DevScene& sc, V3 rd) {
 }
 
 // ---------------------------------------------------------------- camera (generate.rs:24-66)
-__device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, uint32_t* rng) {
+__device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, rt_rng_state* rng) {
     V3 up = ld3(sc.cam_up), right = ld3(sc.right);
     float s_x = sc.x_cf * ((float)x - sc.x_off);
     float s_y = sc.y_cf * ((float)y - sc.y_off);
@@ -1258,7 +931,7 @@ struct Path {
     Ray ray;
     V3 L, T;
     int depth;
-    uint32_t rng;
+    rt_rng_state rng;
     // direct-light sampling (DLS kernels only): a DLS-eligible vertex waits for the next hit,
     // the second index establish_dls_contrib omits (radiance.rs:48-52)
     bool dls_on;
@@ -1388,7 +1061,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
 // Everything of a segment after its closest hit: hit_info, emission, Russian roulette and the
 // continued ray.  Returns true when the path has ended.
 template <bool COUNT, bool GEN, bool DLS>
-__device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& p, Hit h, bool hit, Ctr<COUNT>& c) {
+__device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool hit, Ctr<COUNT>& c) {
     if (DLS && p.dls_on) {  // the previous vertex's DLS term, now that its continued ray has hit
         p.L = p.L + cmul(p.dls_T, dls_contrib(sc, p, hit ? h.ref : REF_NONE));
         p.dls_on = false;
@@ -1405,15 +1078,11 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
     V3 n, pos;
     const DevMat* m;
     if (!GEN || kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
-        float4 s = fetch_sphere<GEN>(sc, k, idx);
+        float4 s = fetch_sphere<GEN>(sc, idx);
         V3 perfect = p.ray.o + p.ray.d * h.l;
         n = normalize(perfect - xyz(s));
         pos = perfect + n * EPS;
-#if RT_LDS_MAT && RT_LDS_SPHERES > 0
         m = GEN ? sc.sph_mat + idx : &g_lds_mat[idx];
-#else
-        m = sc.sph_mat + idx;
-#endif
     } else {  // FreeTriangle hit_info (generic.rs:78-92)
         n = xyz(sc.ftri_n[idx - sc.pool_ftri]);
         pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
@@ -1459,7 +1128,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Cache& k, Path& 
 }
 
 template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false>
-__device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path& p, uint32_t* st,
+__device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true) {
     if (COUNT) c.segments++;
     // The ray's direction arrives un-normalized from camera_ray or shade: one normalize here
@@ -1467,9 +1136,9 @@ __device__ __forceinline__ bool segment(const DevScene& sc, const Cache& k, Path
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop(sc, k, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, k, p.ray, &h, st, c);
+    const bool hit = COOP ? closest_coop(sc, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
-    return shade<COUNT, GEN, DLS>(sc, k, p, h, hit, c);
+    return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
 }
 
 __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, int y, uint32_t pix,
@@ -1490,24 +1159,13 @@ __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, i
 // GEN = false: the scene holds spheres only (and possibly a cube map); triangle and mesh code
 // is compiled out, which keeps the sphere kernel's register budget (walled.yml).
 template <bool COUNT, bool GEN, bool DLS = false>
-#if RT_MIN_WAVES > 0
 __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a) {
-#else
-__global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
-#endif
     extern __shared__ uint32_t dyn_lds[];  // traversal stack: [stack_depth][BLOCK] branch indices
     const DevScene& sc = a.sc;
-    Cache k{0, 0};
-#if RT_LDS_NODES > 0
-    k.n_nodes = sc.n_nodes < (uint32_t)RT_LDS_NODES ? sc.n_nodes : (uint32_t)RT_LDS_NODES;
-    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
-#endif
-#if RT_LDS_SPHERES > 0
-    if (!GEN) fill_lds_spheres(sc, k);  // only the sphere-only kernel reads the LDS sphere tables
-#endif
-#if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
-    if (!GEN || RT_LDS_NODES > 0) __syncthreads();
-#endif
+    if (!GEN) {  // only the sphere-only kernel reads the LDS sphere tables
+        fill_lds_spheres(sc);
+        __syncthreads();
+    }
 
     // workgroup -> tile -> block of 16 x (8/K) pixels, K lanes per pixel (adjacent lanes)
     const uint32_t K = a.lanes_per_pixel;
@@ -1534,7 +1192,7 @@ __global__ __launch_bounds__(BLOCK) void trace_kernel(LaunchArgs a) {
     Path p;
     if (n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk);
     while (i < n_mine) {
-        if (segment<COUNT, GEN, DLS>(sc, k, p, st, c)) {
+        if (segment<COUNT, GEN, DLS>(sc, p, st, c)) {
             const uint32_t rel = kk + K * i;
             if (K == 1) {
                 const float n = (float)(a.sample_begin + rel);  // running mean, draw_scene.rs:81-83
@@ -1638,30 +1296,15 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
 }
 
 template <bool GEN, bool DLS = false>
-#if RT_MIN_WAVES > 0
 __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
-#else
-__global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
-#endif
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
-    Cache k{0, 0};
-#if RT_LDS_NODES > 0
-    k.n_nodes = sc.n_nodes < (uint32_t)RT_LDS_NODES ? sc.n_nodes : (uint32_t)RT_LDS_NODES;
-    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += BLOCK) g_lds_nodes[i] = sc.nodes[i];
-#endif
-#if RT_LDS_SPHERES > 0
-    if (!GEN) fill_lds_spheres(sc, k);  // only the sphere-only kernel reads the LDS sphere tables
-#endif
-#if RT_LDS_NODES > 0 || RT_LDS_SPHERES > 0
-    if (!GEN || RT_LDS_NODES > 0) __syncthreads();
-#endif
-#if RT_GSTACK
+    if (!GEN) {  // only the sphere-only kernel reads the LDS sphere tables
+        fill_lds_spheres(sc);
+        __syncthreads();
+    }
     uint32_t* st = GEN ? dyn_lds + threadIdx.x
                        : a.gstack + (size_t)blockIdx.x * BLOCK * sc.stack_depth + threadIdx.x;
-#else
-    uint32_t* st = dyn_lds + threadIdx.x;
-#endif
     Ctr<false> c;
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
@@ -1670,14 +1313,7 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
-#if RT_TIMING
-    const unsigned long long T_start = RT_CLOCK();
-    unsigned long long t_grab = 0, t_closest = 0, t_shade = 0, iters = 0;
-#endif
     for (;;) {
-#if RT_TIMING
-        const unsigned long long T0 = RT_CLOCK();
-#endif
         const uint64_t need = __ballot(!have && !done);
         // Starting paths is wave-wide work at the width of the idle lanes: in the sphere-only
         // kernel ~10 of 64 lanes end a path per segment, so it waits for RT_REGEN_MIN of them.
@@ -1717,228 +1353,17 @@ __global__ __launch_bounds__(BLOCK) void queue_kernel(LaunchArgs a) {
             }
         }
         if (__ballot(have) == 0) {
-#if RT_TIMING
-            if (lane == 0) atomicAdd(&g_rt_timing[4], RT_CLOCK() - T_start);
-            if (!GEN && lane == 0) {  // sphere-only kernel: [0] item grab + path start, [1] closest, [2] shade
-                atomicAdd(&g_rt_timing[0], t_grab);
-                atomicAdd(&g_rt_timing[1], t_closest);
-                atomicAdd(&g_rt_timing[2], t_shade);
-                atomicAdd(&g_rt_timing[3], iters);
-            }
-#endif
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
-#if RT_TIMING
-        bool fin;
-        if (!GEN) {
-            const unsigned long long T1 = RT_CLOCK();
-            Hit h;
-            bool hit = false;
-            if (have) {
-                p.ray.d = normalize(p.ray.d);  // as segment() does
-                hit = closest<false, GEN>(sc, k, p.ray, &h, st, c);
-            }
-            const unsigned long long T2 = RT_CLOCK();
-            fin = have && shade<false, GEN, DLS>(sc, k, p, h, hit, c);
-            const unsigned long long T3 = RT_CLOCK();
-            t_grab += T1 - T0;
-            t_closest += T2 - T1;
-            t_shade += T3 - T2;
-            ++iters;
-        } else {
-            fin = (GEN && RT_COOP) ? segment<false, GEN, DLS, GEN && RT_COOP>(sc, k, p, st, c, have) && have
-                                   : have && segment<false, GEN, DLS>(sc, k, p, st, c);
-        }
-#else
-        const bool fin = (GEN && RT_COOP) ? segment<false, GEN, DLS, GEN && RT_COOP>(sc, k, p, st, c, have) && have
-                                          : have && segment<false, GEN, DLS>(sc, k, p, st, c);
-#endif
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN>(sc, p, st, c, have) && have
+                                          : have && segment<false, GEN, DLS>(sc, p, st, c);
         if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;
             r[1] = p.L.y;
             r[2] = p.L.z;
             have = false;
-        }
-    }
-}
-
-// ------------------------------------------------------------------ merged traversal loop
-// queue_kernel<true> with RT_COOP ends a segment's traversal when the wave's slowest ray does:
-// lanes that resolved early only help with leaf passes.  Here the loop *is* the traversal: every
-// round each lane descends to its next leaf, the wave tests the leaves cooperatively, and a lane
-// whose traversal resolved shades at once and starts its next ray (or takes a new item) in the
-// next round.  Same per-ray semantics as stack_search (kdtree.rs:66-104).
-template <bool FAST>
-__device__ __forceinline__ void descend_step_loop(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
-                                                  uint32_t& node, int& sp, float& entry, float& exit_t,
-                                                  float& top_t, uint32_t* st, uint2& nd) {
-    nd = fetch_node(sc, k, node);
-    while ((nd.y & 3u) != RT_KD_LEAF) {
-        float d;
-        const float t = split_t<FAST>(nd, ax, r, &d);
-        const bool pos = d > 0.0f;
-        const bool go_near = t >= exit_t;
-        const bool go_far = !go_near && t <= entry;
-        const bool push = !go_near && !go_far;
-        st[sp * BLOCK] = node;
-        sp += push ? 1 : 0;
-        top_t = push ? t : top_t;
-        exit_t = push ? t : exit_t;
-        node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
-        nd = fetch_node(sc, k, node);
-    }
-}
-template <bool FAST>
-__device__ __forceinline__ void pop_far(const DevScene& sc, const Cache& k, const Ray& r, const RayAx& ax,
-                                        uint32_t& node, int& sp, float& entry, float& exit_t, float& top_t,
-                                        float root_exit, uint32_t* st) {
-    --sp;
-    const uint2 pn = fetch_node(sc, k, st[sp * BLOCK]);
-    float d;
-    (void)split_t<FAST>(pn, ax, r, &d);
-    node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
-    entry = top_t;
-    if (sp) {
-        top_t = split_t<FAST>(fetch_node(sc, k, st[(sp - 1) * BLOCK]), ax, r, &d);
-        exit_t = top_t;
-    } else {
-        exit_t = root_exit;
-    }
-}
-
-template <bool DLS>
-#if RT_MIN_WAVES > 0
-__global__ __launch_bounds__(BLOCK, RT_MIN_WAVES_GEN) void merged_kernel(LaunchArgs a) {
-#else
-__global__ __launch_bounds__(BLOCK) void merged_kernel(LaunchArgs a) {
-#endif
-    extern __shared__ uint32_t dyn_lds[];
-    const DevScene& sc = a.sc;
-    const Cache k{0, 0};
-    uint32_t* st = dyn_lds + threadIdx.x;
-    Ctr<false> c;
-    const uint32_t lane = __lane_id();
-    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint32_t pool = 0, pool_end = 0, grab = grab_size<true>(a.n_items, n_waves);
-    bool have = false, qdone = false, need = false, tr = false;
-    uint32_t slot = 0, node = 0;
-    int sp = 0;
-    float entry = 0.f, exit_t = 0.f, top_t = 0.f, root_exit = 0.f;
-    Path p;
-    for (;;) {
-        const uint64_t want = __ballot(!have && !qdone);
-        if (want) {
-            const uint32_t n = (uint32_t)__popcll(want);
-            const uint32_t left = pool_end - pool;
-            uint32_t base = pool_end;
-            if (left < n) {
-                uint32_t b0 = 0;
-                const uint32_t first = (uint32_t)__ffsll((unsigned long long)want) - 1u;
-                if (lane == first) b0 = atomicAdd(a.queue, grab);
-                base = __builtin_amdgcn_readfirstlane(__shfl(b0, first));
-            }
-            if (!have && !qdone) {
-                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-                const uint32_t item = rk < left ? pool + rk : base + (rk - left);
-                if (item < a.n_items) {
-                    uint32_t j, o;
-                    split_item(a, item, &j, &o);
-                    int x, y;
-                    launch_pixel(a, o, &x, &y);
-                    start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
-                    slot = item;
-                    have = true;
-                    need = true;
-                } else {
-                    qdone = true;
-                }
-            }
-            if (left < n) {
-                pool = base + (n - left);
-                pool_end = base + grab;
-                grab = grab_size<true>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
-            } else {
-                pool += n;
-            }
-        }
-        if (__ballot(have) == 0) break;
-
-        bool resolved = false, hit = false;
-        Hit h;
-        if (need) p.ray.d = normalize(p.ray.d);  // arrives un-normalized (see segment())
-        const RayAx ax = ray_axes(p.ray);
-        if (need) {  // a new traversal: root slab test (kdtree.rs:59-61)
-            need = false;
-            float re = 0.f, rx = 0.f;
-            if (sc.n_nodes && entry_exit(sc.bounds, ax, p.ray, &re, &rx)) {
-                tr = true;
-                node = 0;
-                sp = 0;
-                entry = re;
-                exit_t = top_t = root_exit = rx;
-            } else {
-                resolved = true;
-            }
-        }
-        bool fastw = true;
-#if RT_FASTDIV
-        fastw = __ballot(tr && !(sc.fastdiv && origin_fast_ok(p.ray.o))) == 0;
-#else
-        fastw = false;
-#endif
-        uint32_t off = 0, cnt = 0;
-        if (tr) {
-            uint2 nd;
-            if (fastw) descend_step_loop<true>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, st, nd);
-            else descend_step_loop<false>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, st, nd);
-            off = nd.y >> 2;
-            cnt = nd.x;
-        }
-        const unsigned long long key = coop_leaf(sc, p.ray, off, cnt, lane);
-        if (tr) {
-            bool ret = false;
-            if (key != ~0ull) {
-                const uint32_t ref = sc.refs[(uint32_t)key];
-                const float4* pd = prim_data(sc, ref);
-                float l = 0.f, bu = 0.f, bv = 0.f;
-                if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(pd[0], p.ray, &l);
-                else (void)tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), p.ray, &l, &bu, &bv);
-                h.ref = ref;
-                h.l = l;
-                h.bu = bu;
-                h.bv = bv;
-                ret = l <= exit_t + EPS;
-            }
-            if (ret) {
-                tr = false;
-                resolved = hit = true;
-            } else if (sp == 0) {
-                tr = false;
-                resolved = true;
-            } else if (fastw) {
-                pop_far<true>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, root_exit, st);
-            } else {
-                pop_far<false>(sc, k, p.ray, ax, node, sp, entry, exit_t, top_t, root_exit, st);
-            }
-        }
-        if (resolved) {
-            if (!hit && sc.has_cube) {  // unconditional renderables (kdtree.rs:61,103)
-                h.ref = REF_CUBE;
-                h.l = __builtin_inff();
-                hit = true;
-            }
-            if (shade<false, true, DLS>(sc, k, p, h, hit, c)) {
-                float* rr = a.radiance + 3 * (size_t)slot;
-                rr[0] = p.L.x;
-                rr[1] = p.L.y;
-                rr[2] = p.L.z;
-                have = false;
-            } else {
-                need = true;
-            }
         }
     }
 }
@@ -1987,16 +1412,6 @@ __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
     if (a.out) a.out[o] = ov;
 }
 
-#if RT_TIMING
-extern "C" int rt_debug_timing(unsigned long long out[8], int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_timing), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    if (reset) {
-        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt_timing), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#endif
 
 hipError_t launch_fold(const LaunchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(fold_kernel, dim3((a.n_pix + 255) / 256), dim3(256), 0, s, a);
@@ -2020,37 +1435,22 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
 // stack decide): the queue grid is exactly that many workgroups per CU.
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks) {
     const size_t lds = stack_lds_bytes(a);
-#if RT_MERGED && RT_COOP
-    if (!a.sc.spheres_only) {
-        if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, merged_kernel<true>, BLOCK, lds);
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, merged_kernel<false>, BLOCK, lds);
-    }
-#endif
     if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true, true>, BLOCK, lds);
     if (a.sc.spheres_only)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, RT_GSTACK ? 0 : lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, 0);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true>, BLOCK, lds);
 }
 
 size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks) {
-    if (!RT_GSTACK || !a.sc.spheres_only || a.sc.dls) return 0;
+    if (!a.sc.spheres_only || a.sc.dls) return 0;
     return (size_t)n_blocks * BLOCK * a.sc.stack_depth * sizeof(uint32_t);
 }
 
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
-#if RT_MERGED && RT_COOP
-    if (!a.sc.spheres_only) {
-        if (a.sc.dls)
-            hipLaunchKernelGGL((merged_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
-        else
-            hipLaunchKernelGGL((merged_kernel<false>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
-        return hipGetLastError();
-    }
-#endif
     if (a.sc.dls)
         hipLaunchKernelGGL((queue_kernel<true, true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     else if (a.sc.spheres_only)
-        hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), RT_GSTACK ? 0 : stack_lds_bytes(a), s, a);
+        hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), 0, s, a);
     else
         hipLaunchKernelGGL((queue_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();

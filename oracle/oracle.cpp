@@ -72,7 +72,7 @@ static inline M3 mul(const M3& a, const M3& b) {
 // ------------------------------------------------------------------ RNG (src/lib.rs:22-27)
 // The reference's thread_rng() is replaced by the rt_rng.h stream of the current
 // (pixel, sample); every `crate::RNG.with_borrow_mut(|r| r.gen())` is one rng_f32().
-static thread_local uint32_t g_rng;
+static thread_local rt_rng_state g_rng;
 static inline float rng_f32() { return rt_rng_next_f32(&g_rng); }
 
 // ------------------------------------------------------------------ instrumentation
@@ -796,7 +796,15 @@ static V3 dls_contrib(const Scene& s, uint32_t omit0, int omit1, const HitInfo& 
         Ray dr{d, hi.pos};
         Closest c = closest_ray_hit(dr, all.data(), all.size());
         if (c.found && c.elem_idx == i) {
+            // The light's hit_info (radiance.rs:108) seeds a DiffSpec emitter with one draw
+            // (sphere.rs:76, uniform_diff_spec.rs:33-36).  The reference makes that call only
+            // after the whole recursive subtree below the vertex (radiance.rs:44-56), when no
+            // path draw is left, and the emission does not depend on the seed: the draw is
+            // invisible.  Restoring the stream keeps it so in the forward order too, where a
+            // vertex's term is evaluated mid-path.
+            const rt_rng_state saved = g_rng;
             HitInfo lh = s.renderables[i]->hit_info(c.hr, ray);
+            g_rng = saved;
             acc = acc + (light_dot * lh.emissive) * NORMZE;
         }
     }
@@ -1071,7 +1079,7 @@ extern "C" int oracle_triangle_intersect(const float v[9], const float d[3], con
 }
 
 extern "C" void oracle_rng_stream(uint64_t seed, uint32_t pixel, uint64_t sample, uint32_t n, float* out) {
-    uint32_t st = rt_rng_init(seed, pixel, sample);
+    rt_rng_state st = rt_rng_init(seed, pixel, sample);
     for (uint32_t i = 0; i < n; ++i) out[i] = rt_rng_next_f32(&st);
 }
 

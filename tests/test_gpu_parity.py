@@ -128,6 +128,39 @@ def test_dir_light_samp_parity(gpu_available, oracle, scene_name, crop, spp):
         assert float(np.abs(f - plain).max()) > 1e-3  # the crop exercises DLS
 
 
+def test_dir_light_samp_diffspec_emitter(gpu_available, oracle):
+    """DLS towards a DiffSpec emitter: the light's hit_info seeds it with one draw
+    (sphere.rs:76, uniform_diff_spec.rs:33-36), which the reference makes only after the whole
+    recursive subtree (radiance.rs:44-56,108), so it shifts no path draw.  Device, forward oracle
+    and recursive oracle must agree; device == forward oracle bit for bit."""
+    import json
+    import os
+
+    from conftest import SCENES
+    from rt_amd import render, scheme
+
+    d = json.load(open(os.path.join(SCENES, "walled.json")))
+    n_emit = 0
+    for m in d["scene_members"]:
+        mat = m.get("!Sphere", {}).get("mat", {})
+        if "emissive" in mat:
+            mat["divert_ray"] = {"!DiffSpec": {"diffp": 0.6}}
+            n_emit += 1
+    assert n_emit == 2
+    d["render_info"]["rad_info"]["dir_light_samp"] = True
+    sc = scheme.load(d)
+    crop = [(560, 260, 48, 24), (100, 40, 24, 24)]
+    with render.Context(sc) as ctx:
+        g = ctx.render(crop, 0, 12)
+    f = oracle.render(sc, crop, 0, 12, accum=oracle.ACCUM_FORWARD)
+    r = oracle.render(sc, crop, 0, 12, accum=oracle.ACCUM_RECURSIVE)
+    sf, sr = parity.stats(g, f), parity.stats(g, r)
+    print("diffspec emitter: vs forward", sf, "\n vs recursive", sr)
+    assert np.array_equal(g, f), sf
+    assert sr["frac_ok"] >= parity.MIN_FRAC, sr
+    assert sr["mean_rel_err"] < 1e-3
+
+
 def test_dir_light_samp_schedules_agree(gpu_available, monkeypatch):
     from rt_amd import render
 

@@ -1,0 +1,105 @@
+"""Parity at the production launch shapes: the device renders whole frames exactly as bench.py
+and the scheme configs launch them (full-frame queue launches, the configs' resolutions, sample
+offsets and batch sizes), and scattered pixels of the result are compared bit for bit with the
+forward oracle run on just those pixels.  Reference loop: render_to_target_cpu
+(src/render/draw_scene.rs:71-98)."""
+import numpy as np
+import pytest
+
+import parity
+from conftest import load_scene
+
+pytestmark = pytest.mark.gpu
+
+
+def scattered(w, h, n, seed, extra=()):
+    """n distinct pixels of a w x h frame (seeded), plus the corners and the centre."""
+    rng = np.random.default_rng(seed)
+    pts = {(0, 0), (w - 1, 0), (0, h - 1), (w - 1, h - 1), (w // 2, h // 2)} | set(extra)
+    while len(pts) < n:
+        pts.add((int(rng.integers(0, w)), int(rng.integers(0, h))))
+    return sorted(pts, key=lambda p: (p[1], p[0]))
+
+
+def pick(frame, w, pts):
+    return np.stack([frame[y * w + x] for (x, y) in pts])
+
+
+def test_walled_bench_launch_shape(gpu_available, oracle):
+    """walled.yml as bench.py's step runs it: one full-frame 1000-spp queue launch (720 M items),
+    here at sample_begin 19000 (the 20th step of the 20000-spp scheme)."""
+    from rt_amd import render
+
+    sc = load_scene("walled")
+    w, h = int(sc.info.width), int(sc.info.height)
+    pts = scattered(w, h, 256, seed=19)
+    with render.Context(sc) as ctx:
+        frame = ctx.render(None, 19000, 1000)
+        n_launch = ctx.launch_stats()["n_trace_launches"]
+    assert n_launch == 1  # one queue launch, as in the bench
+    g = pick(frame, w, pts)
+    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 19000, 1000, accum=oracle.ACCUM_FORWARD)
+    s = parity.stats(g, o)
+    print("walled 1000 spp @19000", s)
+    assert np.array_equal(g, o), s
+
+
+def test_spaceship_4096_config5(gpu_available, oracle):
+    """spaceship_r1.yml at 4096 x 4096 (BASELINE config 5): the full frame at 4 spp in the
+    scheme's batches of 25 -> here one call, 64 scattered pixels plus two 32 x 32 tiles."""
+    from rt_amd import render
+
+    sc = load_scene("spaceship_r1", width=4096, height=4096)
+    w, h = 4096, 4096
+    pts = scattered(w, h, 64, seed=5)
+    blocks = [(2040, 2040, 32, 32), (1500, 2600, 32, 32)]
+    with render.Context(sc) as ctx:
+        frame = ctx.render(None, 0, 4)
+    g = pick(frame, w, pts)
+    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 0, 4, accum=oracle.ACCUM_FORWARD)
+    s = parity.stats(g, o)
+    print("spaceship 4096^2 scattered", s)
+    assert np.array_equal(g, o), s
+    img = frame.reshape(h, w, 4)
+    gb = np.concatenate([img[y:y + bh, x:x + bw].reshape(-1, 4) for (x, y, bw, bh) in blocks])
+    ob = oracle.render(sc, blocks, 0, 4, accum=oracle.ACCUM_FORWARD)
+    sb = parity.stats(gb, ob)
+    print("spaceship 4096^2 blocks", sb)
+    assert np.array_equal(gb, ob), sb
+    assert (img[..., 3] == 1.0).all()
+
+
+def test_biplane_200spp_scheme_batches(gpu_available, oracle):
+    """biplane.yml at BASELINE config 3's 200 spp, in the scheme's gpu_render_batch of 10
+    (20 full-frame launches, the running mean carried across them)."""
+    from rt_amd import render
+
+    sc = load_scene("biplane")
+    w, h = int(sc.info.width), int(sc.info.height)
+    pts = scattered(w, h, 128, seed=3, extra=((600, 300), (610, 310)))
+    with render.Context(sc) as ctx:
+        for s0 in range(0, 200, 10):
+            frame = ctx.render(None, s0, 10, want_output=(s0 == 190))
+    g = pick(frame, w, pts)
+    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 0, 200, accum=oracle.ACCUM_FORWARD)
+    s = parity.stats(g, o)
+    print("biplane 200 spp", s)
+    assert np.array_equal(g, o), s
+
+
+def test_a380_batch1(gpu_available, oracle):
+    """a380.yml (synthetic stand-in geometry) at its own gpu_render_batch of 1: ten one-sample
+    full-frame launches."""
+    from rt_amd import render
+
+    sc = load_scene("a380")
+    w, h = int(sc.info.width), int(sc.info.height)
+    pts = scattered(w, h, 96, seed=38)
+    with render.Context(sc) as ctx:
+        for s0 in range(10):
+            frame = ctx.render(None, s0, 1, want_output=(s0 == 9))
+    g = pick(frame, w, pts)
+    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 0, 10, accum=oracle.ACCUM_FORWARD)
+    s = parity.stats(g, o)
+    print("a380 batch 1", s)
+    assert np.array_equal(g, o), s
