@@ -31,12 +31,36 @@ using namespace rth;
 // (4 GiB cap).  RT_QUEUE_RADIANCE_GIB overrides it; only what a launch needs is allocated.
 static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 
+// The queue launches alternate between two pipeline slots, each with its own stream, radiance
+// buffer, item counter and traversal-stack scratch: launch i + 1 starts while launch i drains
+// (its last paths finish on a few lanes), and only the folds, which update the shared
+// accumulators and the output, are chained in order by events.
+constexpr int N_SLOTS = 2;
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t fold_done = nullptr;   // this slot's last fold (its radiance buffer is free again)
+    float* radiance = nullptr;
+    uint64_t radiance_cap = 0;        // floats
+    uint32_t* queue = nullptr;        // queue schedule item counter
+    uint32_t* gstack = nullptr;       // sphere-only queue kernel's traversal stacks (queue_gstack_bytes)
+    size_t gstack_cap = 0;
+};
+
 struct rt_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::vector<hipEvent_t> lev;  // start/stop pairs around each trace launch of the last call
+    hipStream_t stream = nullptr;     // = slot[0].stream: uploads, synchronous paths
+    Slot slot[N_SLOTS];
+    uint32_t next_slot = 0;
+    hipEvent_t last_fold = nullptr;   // the most recent fold enqueued (nullptr: none pending)
+    hipEvent_t caller_ev = nullptr;   // the caller's stream, recorded at an async call
+    // Timing window: every trace launch since the window opened, as start / stop event pairs,
+    // and the whole window from its first launch to its last fold (closed by rt_synchronize
+    // or at the end of a synchronous call).
+    std::vector<hipEvent_t> lev;
     uint32_t n_launch = 0;
+    hipEvent_t win_end = nullptr;     // the window's last event (win_end_ev or a launch stop)
+    hipEvent_t win_end_ev = nullptr;
+    bool pending = false;             // enqueued work not yet synchronised
     float trace_ms = 0.f;
     DevScene sc{};
     std::vector<void*> allocs;
@@ -49,16 +73,12 @@ struct rt_ctx {
     float4* d_out = nullptr;
     uint64_t d_out_cap = 0;
     DevCounts* d_counts = nullptr;
-    float* radiance = nullptr;    // K > 1 sample buffer
-    uint64_t radiance_cap = 0;    // floats
     uint64_t lane_capacity = 0;   // lanes resident at the kernel's occupancy
     uint32_t n_cu = 0;
     uint32_t forced_k = 0;        // RT_LANES_PER_PIXEL (tests / tuning)
-    uint32_t* d_queue = nullptr;  // queue schedule item counter
-    uint32_t* gstack = nullptr;   // sphere-only queue kernel's traversal stacks (queue_gstack_bytes)
-    size_t gstack_cap = 0;
     int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
     uint64_t queue_floats = 0;    // RT_QUEUE_RADIANCE_GIB: radiance buffer cap per queue launch
+    bool overlap = true;          // RT_PIPELINE: launch i + 1 may start during launch i's drain
     float last_ms = 0.f;
     std::string err;
 };
@@ -125,19 +145,23 @@ static DevMat make_mat(const rt_material& m, const float rgb[3]) {
 static void destroy_ctx(rt_ctx* c) {
     if (!c) return;
     if (c->stream) (void)hipSetDevice(c->device);
+    for (Slot& sl : c->slot) if (sl.stream) (void)hipStreamSynchronize(sl.stream);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->accum) (void)hipFree(c->accum);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     if (c->d_pixmap) (void)hipFree(c->d_pixmap);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_counts) (void)hipFree(c->d_counts);
-    if (c->d_queue) (void)hipFree(c->d_queue);
-    if (c->gstack) (void)hipFree(c->gstack);
-    if (c->radiance) (void)hipFree(c->radiance);
+    for (Slot& sl : c->slot) {
+        if (sl.queue) (void)hipFree(sl.queue);
+        if (sl.gstack) (void)hipFree(sl.gstack);
+        if (sl.radiance) (void)hipFree(sl.radiance);
+        if (sl.fold_done) (void)hipEventDestroy(sl.fold_done);
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
+    }
     for (hipEvent_t e : c->lev) (void)hipEventDestroy(e);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
+    if (c->win_end_ev) (void)hipEventDestroy(c->win_end_ev);
     delete c;
 }
 
@@ -208,6 +232,16 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
             n.y = (at << 2) | RT_KD_LEAF;
         }
         refs.swap(packed);
+    }
+    // Leading sphere refs of every leaf (device_scene.h LEAF_LEAD_SHIFT): the general kernel
+    // tests them per lane and leaves only triangles to the wave's cooperative passes.
+    for (uint2& n : nodes) {
+        if ((n.y & 3u) != RT_KD_LEAF) continue;
+        if (n.x > LEAF_COUNT_MASK) return set_err(c, RT_ERR_UNSUPPORTED, "KD leaf with over 2^24 refs");
+        const uint32_t off = n.y >> 2;
+        uint32_t lead = 0;
+        while (lead < n.x && lead < 255u && (refs[off + lead] >> REF_KIND_SHIFT) == K_SPHERE) ++lead;
+        n.x |= lead << LEAF_LEAD_SHIFT;
     }
 
     // Direct-light sampling (radiance.rs:89-120): every AABB'd renderable as a device ref in
@@ -308,9 +342,14 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
 
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(c, hipEventCreate(&c->ev0));
-    HIPCHK(c, hipEventCreate(&c->ev1));
+    for (Slot& sl : c->slot) {
+        HIPCHK(c, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&sl.fold_done, hipEventDisableTiming));
+        if (hipMalloc(&sl.queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
+    }
+    c->stream = c->slot[0].stream;
+    HIPCHK(c, hipEventCreateWithFlags(&c->caller_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreate(&c->win_end_ev));
     if ((st = upload(c, nodes, &d.nodes))) return st;
     if ((st = upload(c, elem_refs, &d.elem_refs))) return st;
     if ((st = upload(c, emit, &d.emit))) return st;
@@ -328,6 +367,13 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         for (uint32_t i = 0; i < scene->n_spheres; ++i) pool[3 * (size_t)i] = sph[i];
         std::memcpy(pool.data() + 3 * (size_t)scene->n_spheres, ftri.data(), ftri.size() * sizeof(float4));
         if (n_mesh) std::memcpy(pool.data() + 3 * ((size_t)scene->n_spheres + scene->n_free_tris), mf.verts.data(), 3 * n_mesh * sizeof(float4));
+        // triangles as {v0, e1 = v1 - v0, e2 = v2 - v0}: generic.rs:104-105's edges, the same f32
+        // subtractions the device would make per test
+        for (size_t t = scene->n_spheres; t < pool.size() / 3; ++t) {
+            const float4 v0 = pool[3 * t], v1 = pool[3 * t + 1], v2 = pool[3 * t + 2];
+            pool[3 * t + 1] = make_float4(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z, 0.f);
+            pool[3 * t + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.f);
+        }
         if ((st = upload(c, pool, &d.prim4))) return st;
         d.pool_ftri = scene->n_spheres;
         d.pool_mesh = scene->n_spheres + scene->n_free_tris;
@@ -409,7 +455,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
     c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
     c->n_cu = (uint32_t)prop.multiProcessorCount;
-    if (hipMalloc(&c->d_queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
     if (const char* e = std::getenv("RT_SCHED")) {
         if (!std::strcmp(e, "direct")) c->sched = 1;
         else if (!std::strcmp(e, "queue")) c->sched = 2;
@@ -423,6 +468,16 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->queue_floats = (uint64_t)v << 28;
     }
+    // Traversal of the queue kernels: the reference's stack (kdtree.rs:66-104) or stackless
+    // kd-restart with push-down, bit-identical (trace.hip stack_search_coop).  The stack is faster
+    // on the mesh scenes; the sphere-only kernel, which descends for 0.05 nodes
+    // per sample, runs stackless and needs no global stack.  RT_KD_RESTART=0/1 overrides.
+    d.restart = d.spheres_only ? 1u : 0u;
+    if (const char* e = std::getenv("RT_KD_RESTART")) d.restart = std::strcmp(e, "0") != 0 ? 1u : 0u;
+    // Overlapped launches pay off where the drain tail is long (mesh scenes: 8-10 ms per launch,
+    // DESIGN.md §8); the sphere-only kernel's is ~0.4 ms.  RT_PIPELINE=0/1 overrides.
+    c->overlap = !d.spheres_only;
+    if (const char* e = std::getenv("RT_PIPELINE")) c->overlap = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("RT_QUEUE_RADIANCE_FLOATS")) {  // tests: force split launches
         unsigned long long v = std::strtoull(e, nullptr, 10);
         if (v >= 3 && v <= (1ull << 34)) c->queue_floats = (uint64_t)v;
@@ -450,7 +505,48 @@ extern "C" int rt_create(const rt_scene_desc* scene, const rt_camera* cam, const
     return RT_OK;
 }
 
-// Builds the per-launch tile table; returns the number of output pixels.
+// Drains both pipeline slots and closes the timing window: per-launch trace durations and the
+// window's span, from its first trace launch to its last fold.
+static int sync_all(rt_ctx* c) {
+    for (Slot& sl : c->slot) HIPCHK(c, hipStreamSynchronize(sl.stream));
+    if (!c->pending) return RT_OK;
+    c->pending = false;
+    c->trace_ms = 0.f;
+    for (uint32_t i = 0; i < c->n_launch; ++i) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->lev[2 * i], c->lev[2 * i + 1]));
+        c->trace_ms += ms;
+    }
+    c->last_ms = 0.f;
+    if (c->n_launch && c->win_end) HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->lev[0], c->win_end));
+    return RT_OK;
+}
+
+// Opens a new timing window unless one is pending (async calls extend it).
+static void open_window(rt_ctx* c) {
+    if (c->pending) return;
+    c->pending = true;
+    c->n_launch = 0;
+    c->win_end = nullptr;
+}
+
+// An event from the pool: launch i's start (begin) or stop, recorded on `s`.
+static int record_launch_event(rt_ctx* c, bool begin, hipStream_t s, hipEvent_t* out = nullptr) {
+    const size_t i = 2 * (size_t)c->n_launch + (begin ? 0 : 1);
+    while (c->lev.size() <= i) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->lev.push_back(e);
+    }
+    HIPCHK(c, hipEventRecord(c->lev[i], s));
+    if (out) *out = c->lev[i];
+    if (!begin) c->n_launch++;
+    return RT_OK;
+}
+
+// Builds the per-launch tile table (and the pixel table) unless the same tiles are already on
+// the device; returns the number of output pixels.  New tiles drain the pipeline first, since a
+// launch in flight may read the old tables.
 static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint32_t K, LaunchArgs* a,
                          uint64_t* n_out) {
     if (!tiles || n_tiles == 0) return set_err(c, RT_ERR_INVALID_ARG, "no tiles");
@@ -470,27 +566,27 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
         pix += (uint64_t)t.w * t.h;
     }
     if (blocks >= (1ull << 31) || pix >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels");
-    if (n_tiles > c->d_tiles_cap) {
-        if (c->d_tiles) (void)hipFree(c->d_tiles);
-        c->d_tiles = nullptr;
-        c->d_tiles_cap = 0;
-        if (hipMalloc(&c->d_tiles, n_tiles * sizeof(DevTile)) != hipSuccess) return set_err(c, RT_ERR_OOM, "tile alloc failed");
-        c->d_tiles_cap = n_tiles;
-    }
-    HIPCHK(c, hipMemcpyAsync(c->d_tiles, dt.data(), n_tiles * sizeof(DevTile), hipMemcpyHostToDevice, c->stream));
-    // A per-pixel table replaces the per-item binary search over the tiles (whose dependent
-    // loads held back every wave that started a path: rank 0 of 8 with 1-row stripes ran 8%
-    // slower) and the divisions by the tile width.  Kept while the same tiles come back.
-    a->pix_xy = nullptr;
-    if (c->sc.width <= 65535u && c->sc.height <= 65535u) {
-        const bool same = c->pixmap_tiles.size() == dt.size() &&
-                          std::memcmp(c->pixmap_tiles.data(), dt.data(), dt.size() * sizeof(DevTile)) == 0;
-        if (!same) {
+    const bool same = c->pixmap_tiles.size() == dt.size() &&
+                      std::memcmp(c->pixmap_tiles.data(), dt.data(), dt.size() * sizeof(DevTile)) == 0;
+    if (!same) {
+        int st = sync_all(c);
+        if (st) return st;
+        if (n_tiles > c->d_tiles_cap) {
+            if (c->d_tiles) (void)hipFree(c->d_tiles);
+            c->d_tiles = nullptr;
+            c->d_tiles_cap = 0;
+            if (hipMalloc(&c->d_tiles, n_tiles * sizeof(DevTile)) != hipSuccess) return set_err(c, RT_ERR_OOM, "tile alloc failed");
+            c->d_tiles_cap = n_tiles;
+        }
+        HIPCHK(c, hipMemcpy(c->d_tiles, dt.data(), n_tiles * sizeof(DevTile), hipMemcpyHostToDevice));
+        // A per-pixel table replaces the per-item binary search over the tiles (whose dependent
+        // loads held back every wave that started a path: rank 0 of 8 with 1-row stripes ran 8%
+        // slower) and the divisions by the tile width.
+        if (c->sc.width <= 65535u && c->sc.height <= 65535u) {
             std::vector<uint32_t> pm(pix);
             for (const DevTile& d : dt)
                 for (uint32_t y = 0; y < d.h; ++y)
                     for (uint32_t x = 0; x < d.w; ++x) pm[d.out_off + (size_t)y * d.w + x] = ((d.y0 + y) << 16) | (d.x0 + x);
-            HIPCHK(c, hipStreamSynchronize(c->stream));  // a running launch may read the old table
             if (pix > c->d_pixmap_cap) {
                 if (c->d_pixmap) (void)hipFree(c->d_pixmap);
                 c->d_pixmap = nullptr;
@@ -499,10 +595,10 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                 c->d_pixmap_cap = pix;
             }
             HIPCHK(c, hipMemcpy(c->d_pixmap, pm.data(), pix * sizeof(uint32_t), hipMemcpyHostToDevice));
-            c->pixmap_tiles = dt;
         }
-        a->pix_xy = c->d_pixmap;
+        c->pixmap_tiles = dt;
     }
+    a->pix_xy = (c->sc.width <= 65535u && c->sc.height <= 65535u) ? c->d_pixmap : nullptr;
     a->sc = c->sc;
     a->tiles = c->d_tiles;
     a->n_tiles = n_tiles;
@@ -515,7 +611,11 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
     return RT_OK;
 }
 
-static uint64_t tile_pixels(const rt_tile* tiles, uint32_t n);
+static uint64_t tile_pixels(const rt_tile* tiles, uint32_t n) {
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < n; ++i) p += (uint64_t)tiles[i].w * tiles[i].h;
+    return p;
+}
 
 // Lanes per pixel: enough (pixel, sample-stream) lanes to fill the chip ~1.5x at the kernel's
 // occupancy; 1 whenever the launch has that many pixels (then samples fold in registers).
@@ -526,14 +626,17 @@ static uint32_t choose_k(const rt_ctx* c, uint64_t n_pix) {
     return k;
 }
 
-static int ensure_radiance(rt_ctx* c, uint64_t floats) {
-    if (floats <= c->radiance_cap) return RT_OK;
-    if (c->radiance) (void)hipFree(c->radiance);
-    c->radiance = nullptr;
-    c->radiance_cap = 0;
-    if (hipMalloc(&c->radiance, floats * sizeof(float)) != hipSuccess)
+// A slot's radiance buffer of at least `floats`; the slot's stream is drained before a
+// reallocation (a launch of its own may still be writing the old buffer).
+static int ensure_radiance(rt_ctx* c, Slot& sl, uint64_t floats) {
+    if (floats <= sl.radiance_cap) return RT_OK;
+    HIPCHK(c, hipStreamSynchronize(sl.stream));
+    if (sl.radiance) (void)hipFree(sl.radiance);
+    sl.radiance = nullptr;
+    sl.radiance_cap = 0;
+    if (hipMalloc(&sl.radiance, floats * sizeof(float)) != hipSuccess)
         return set_err(c, RT_ERR_OOM, "radiance buffer alloc failed");
-    c->radiance_cap = floats;
+    sl.radiance_cap = floats;
     return RT_OK;
 }
 
@@ -543,131 +646,140 @@ static constexpr uint32_t SAMPLES_PER_LANE_CHUNK = 64;
 // walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_SCHED=direct or
 // RT_LANES_PER_PIXEL asks for the direct one-lane-per-pixel schedule (kept for A/B and as the
 // tests' second path).
-static bool use_queue(const rt_ctx* c, uint64_t n_pix) {
-    (void)n_pix;
+static bool use_queue(const rt_ctx* c) {
     if (c->forced_k) return false;
     return c->sched != 1;
 }
 
-// Records the start (begin) or stop event of the current trace launch.
-static int mark_launch(rt_ctx* c, bool begin) {
-    const size_t i = 2 * (size_t)c->n_launch + (begin ? 0 : 1);
-    while (c->lev.size() <= i) {
-        hipEvent_t e;
-        HIPCHK(c, hipEventCreate(&e));
-        c->lev.push_back(e);
+// Queue schedule, asynchronous: each chunk of samples (bounded by the radiance cap) is one
+// trace launch on the next pipeline slot, followed on the same stream by its fold.  The trace
+// waits only for its slot's previous fold (same stream); the fold also waits for the previous
+// chunk's fold (accumulator order, draw_scene.rs:81-83) and, when given, for `after` (the
+// caller's stream: its readers of `out` from the previous call).  Returns with the last fold
+// in c->last_fold.
+static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sample_begin,
+                         uint32_t sample_count, hipEvent_t after) {
+    uint64_t chunk = c->queue_floats / (3 * n_out);
+    if (chunk < 1) chunk = 1;
+    if (chunk > sample_count) chunk = sample_count ? sample_count : 1;
+    int per_cu = 0;  // the queue grid: the resident workgroups of this scene's kernel
+    HIPCHK(c, queue_blocks_per_cu(a, &per_cu));
+    if (per_cu < 1) per_cu = 1;
+    const uint64_t lanes = (uint64_t)c->n_cu * (uint64_t)per_cu * BLOCK;
+    // the counter overshoots n_items by at most one grab (<= 1024 = 16 x 64) per wave
+    if (n_out * chunk + lanes * 16 >= (1ull << 32)) chunk = ((1ull << 32) - lanes * 16 - 1) / n_out;
+    if (chunk < 1) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels for one launch");
+    if (sample_count > chunk) {  // equal launches: ceil(count / n) samples each
+        const uint64_t n = (sample_count + chunk - 1) / chunk;
+        chunk = (sample_count + n - 1) / n;
     }
-    HIPCHK(c, hipEventRecord(c->lev[i], c->stream));
-    if (!begin) c->n_launch++;
-    return RT_OK;
-}
-
-// After the stream has drained: total time and the trace launches' share.
-static int finish_timing(rt_ctx* c) {
-    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    c->trace_ms = 0.f;
-    for (uint32_t i = 0; i < c->n_launch; ++i) {
-        float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->lev[2 * i], c->lev[2 * i + 1]));
-        c->trace_ms += ms;
-    }
-    return RT_OK;
-}
-
-static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
-                       uint32_t sample_count, float4* dev_out) {
-    LaunchArgs a{};
-    uint64_t n_out = 0;
-    const uint32_t K = choose_k(c, tile_pixels(tiles, n_tiles));
-    int st = prepare_tiles(c, tiles, n_tiles, K, &a, &n_out);
-    if (st) return st;
-    a.out = dev_out;
-    c->n_launch = 0;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if (use_queue(c, n_out)) {
-        uint64_t chunk = c->queue_floats / (3 * n_out);
-        if (chunk < 1) chunk = 1;
-        if (chunk > sample_count) chunk = sample_count ? sample_count : 1;
-        int per_cu = 0;  // the queue grid: the resident workgroups of this scene's kernel
-        HIPCHK(c, queue_blocks_per_cu(a, &per_cu));
-        if (per_cu < 1) per_cu = 1;
-        const uint64_t lanes = (uint64_t)c->n_cu * (uint64_t)per_cu * BLOCK;
-        // the counter overshoots n_items by at most one grab (<= 1024 = 16 x 64) per wave
-        if ((uint64_t)n_out * chunk + lanes * 16 >= (1ull << 32)) chunk = ((1ull << 32) - lanes * 16 - 1) / n_out;
-        if (chunk < 1) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels for one launch");
-        if (sample_count > chunk) {  // equal launches: ceil(count / n) samples each
-            const uint64_t n = (sample_count + chunk - 1) / chunk;
-            chunk = (sample_count + n - 1) / n;
-        }
-        if ((st = ensure_radiance(c, 3 * n_out * chunk))) return st;
-        a.radiance = c->radiance;
+    uint32_t done = 0;
+    do {
+        Slot& sl = c->slot[c->next_slot];
+        c->next_slot = (c->next_slot + 1) % N_SLOTS;
+        a.sample_begin = sample_begin + done;
+        a.sample_count = (uint32_t)(sample_count - done < chunk ? sample_count - done : chunk);
+        a.n_items = (uint32_t)(n_out * a.sample_count);
+        int st = ensure_radiance(c, sl, 3 * n_out * (a.sample_count ? a.sample_count : 1));
+        if (st) return st;
+        a.radiance = sl.radiance;
+        a.queue = sl.queue;
         a.gstack = nullptr;
         if (const size_t gb = queue_gstack_bytes(a, (uint32_t)(lanes / BLOCK))) {
-            if (gb > c->gstack_cap) {
-                if (c->gstack) (void)hipFree(c->gstack);
-                c->gstack = nullptr;
-                c->gstack_cap = 0;
-                if (hipMalloc(&c->gstack, gb) != hipSuccess) return set_err(c, RT_ERR_OOM, "traversal stack alloc failed");
-                c->gstack_cap = gb;
+            if (gb > sl.gstack_cap) {
+                HIPCHK(c, hipStreamSynchronize(sl.stream));
+                if (sl.gstack) (void)hipFree(sl.gstack);
+                sl.gstack = nullptr;
+                sl.gstack_cap = 0;
+                if (hipMalloc(&sl.gstack, gb) != hipSuccess) return set_err(c, RT_ERR_OOM, "traversal stack alloc failed");
+                sl.gstack_cap = gb;
             }
-            a.gstack = c->gstack;
+            a.gstack = sl.gstack;
         }
-        a.queue = c->d_queue;
-        uint32_t done = 0;
-        do {
-            a.sample_begin = sample_begin + done;
-            a.sample_count = (uint32_t)(sample_count - done < chunk ? sample_count - done : chunk);
-            a.n_items = (uint32_t)(n_out * a.sample_count);
-            if (a.sample_count) {
-                HIPCHK(c, hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), c->stream));
-                if ((st = mark_launch(c, true))) return st;
-                HIPCHK(c, launch_trace_queue(a, (uint32_t)(lanes / BLOCK), c->stream));
-                if ((st = mark_launch(c, false))) return st;
-            }
-            HIPCHK(c, launch_fold(a, c->stream));
-            done += a.sample_count;
-        } while (done < sample_count);
-    } else if (K == 1) {
+        // Without overlap the trace also waits for the previous fold: the sphere-only kernel's
+        // drain tail is ~0.4 ms, and a fold beside the next persistent trace grid cost walled 2%
+        // (its workgroups take slots from that grid).
+        if (!c->overlap && c->last_fold && c->last_fold != sl.fold_done)
+            HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));
+        if (a.sample_count) {
+            HIPCHK(c, hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), sl.stream));
+            if ((st = record_launch_event(c, true, sl.stream))) return st;
+            HIPCHK(c, launch_trace_queue(a, (uint32_t)(lanes / BLOCK), sl.stream));
+            if ((st = record_launch_event(c, false, sl.stream))) return st;
+        }
+        if (c->last_fold && c->last_fold != sl.fold_done) HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));
+        if (after) HIPCHK(c, hipStreamWaitEvent(sl.stream, after, 0));
+        HIPCHK(c, launch_fold(a, sl.stream));
+        HIPCHK(c, hipEventRecord(sl.fold_done, sl.stream));
+        c->last_fold = sl.fold_done;
+        done += a.sample_count;
+    } while (done < sample_count);
+    // the window ends at this fold (fold_done carries no timestamp)
+    HIPCHK(c, hipEventRecord(c->win_end_ev, c->slot[(c->next_slot + N_SLOTS - 1) % N_SLOTS].stream));
+    c->win_end = c->win_end_ev;
+    return RT_OK;
+}
+
+// Direct schedule (trace_kernel), synchronous on slot 0 after draining the pipeline.
+static int run_direct(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint32_t K, uint64_t sample_begin,
+                      uint32_t sample_count) {
+    int st = sync_all(c);
+    if (st) return st;
+    open_window(c);
+    Slot& sl = c->slot[0];
+    if (K == 1) {
         a.sample_begin = sample_begin;
         a.sample_count = sample_count;
-        if ((st = mark_launch(c, true))) return st;
-        HIPCHK(c, launch_trace(a, c->stream));  // count 0 still (re)writes the accumulators
-        if ((st = mark_launch(c, false))) return st;
+        if ((st = record_launch_event(c, true, sl.stream))) return st;
+        HIPCHK(c, launch_trace(a, sl.stream));  // count 0 still (re)writes the accumulators
+        if ((st = record_launch_event(c, false, sl.stream, &c->win_end))) return st;
     } else {
         const uint32_t chunk = sample_count < SAMPLES_PER_LANE_CHUNK * K ? sample_count : SAMPLES_PER_LANE_CHUNK * K;
-        if ((st = ensure_radiance(c, 3 * n_out * (chunk ? chunk : 1)))) return st;
-        a.radiance = c->radiance;
+        if ((st = ensure_radiance(c, sl, 3 * n_out * (chunk ? chunk : 1)))) return st;
+        a.radiance = sl.radiance;
         uint32_t done = 0;
         do {
             a.sample_begin = sample_begin + done;
             a.sample_count = sample_count - done < chunk ? sample_count - done : chunk;
             if (a.sample_count) {
-                if ((st = mark_launch(c, true))) return st;
-                HIPCHK(c, launch_trace(a, c->stream));
-                if ((st = mark_launch(c, false))) return st;
+                if ((st = record_launch_event(c, true, sl.stream))) return st;
+                HIPCHK(c, launch_trace(a, sl.stream));
+                if ((st = record_launch_event(c, false, sl.stream, &c->win_end))) return st;
             }
-            HIPCHK(c, launch_fold(a, c->stream));
+            HIPCHK(c, launch_fold(a, sl.stream));
             done += a.sample_count;
         } while (done < sample_count);
     }
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(sl.fold_done, sl.stream));
+    c->last_fold = sl.fold_done;
+    c->next_slot = 1 % N_SLOTS;
     return RT_OK;
+}
+
+// Enqueues one rt_render* call.  `after`: an event the output writers must wait for.
+static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                       uint32_t sample_count, float4* dev_out, hipEvent_t after) {
+    LaunchArgs a{};
+    uint64_t n_out = 0;
+    const uint32_t K = choose_k(c, tile_pixels(tiles, n_tiles));
+    int st = prepare_tiles(c, tiles, n_tiles, use_queue(c) ? 1 : K, &a, &n_out);
+    if (st) return st;
+    a.out = dev_out;
+    if (!use_queue(c)) return run_direct(c, a, n_out, K, sample_begin, sample_count);
+    open_window(c);
+    return enqueue_queue(c, a, n_out, sample_begin, sample_count, after);
 }
 
 static int ensure_out(rt_ctx* c, uint64_t n) {
     if (n <= c->d_out_cap) return RT_OK;
+    int st = sync_all(c);
+    if (st) return st;
     if (c->d_out) (void)hipFree(c->d_out);
     c->d_out = nullptr;
     c->d_out_cap = 0;
     if (hipMalloc(&c->d_out, n * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "output alloc failed");
     c->d_out_cap = n;
     return RT_OK;
-}
-
-static uint64_t tile_pixels(const rt_tile* tiles, uint32_t n) {
-    uint64_t p = 0;
-    for (uint32_t i = 0; i < n; ++i) p += (uint64_t)tiles[i].w * tiles[i].h;
-    return p;
 }
 
 extern "C" int rt_render(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
@@ -677,21 +789,49 @@ extern "C" int rt_render(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
     const uint64_t n = tile_pixels(tiles, n_tiles);
     int st;
     if (out_rgba && (st = ensure_out(c, n))) return st;
-    if ((st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, out_rgba ? c->d_out : nullptr))) return st;
-    if (out_rgba)
-        HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return finish_timing(c);
+    if ((st = sync_all(c))) return st;  // a synchronous call is its own timing window
+    if ((st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, out_rgba ? c->d_out : nullptr, nullptr))) return st;
+    if (out_rgba)  // on the stream of the last fold
+        HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost,
+                                 c->slot[(c->next_slot + N_SLOTS - 1) % N_SLOTS].stream));
+    return sync_all(c);
+}
+
+extern "C" int rt_render_device_async(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles,
+                                      uint64_t sample_begin, uint32_t sample_count, float* out_dev,
+                                      void* stream) {
+    if (!c || !tiles || !out_dev) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    // the caller's work enqueued so far (e.g. a gather still reading out_dev) precedes the folds
+    HIPCHK(c, hipEventRecord(c->caller_ev, cs));
+    int st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, reinterpret_cast<float4*>(out_dev),
+                         c->caller_ev);
+    if (st) return st;
+    // and the caller's later work sees the finished output
+    HIPCHK(c, hipStreamWaitEvent(cs, c->last_fold, 0));
+    return RT_OK;
 }
 
 extern "C" int rt_render_device(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles,
                                 uint64_t sample_begin, uint32_t sample_count, float* out_dev) {
     if (!c || !tiles || !out_dev) return RT_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    int st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, reinterpret_cast<float4*>(out_dev));
+    int st = sync_all(c);
     if (st) return st;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return finish_timing(c);
+    // ordered after the legacy default stream's work (e.g. the caller's allocation / clearing of
+    // out_dev), and complete on return
+    HIPCHK(c, hipEventRecord(c->caller_ev, nullptr));
+    if ((st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, reinterpret_cast<float4*>(out_dev),
+                          c->caller_ev)))
+        return st;
+    return sync_all(c);
+}
+
+extern "C" int rt_synchronize(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    return sync_all(c);
 }
 
 extern "C" int rt_last_kernel_ms(const rt_ctx* c, float* ms) {
@@ -718,9 +858,11 @@ extern "C" int rt_count_work_ex(rt_ctx* c, const rt_tile* tiles, uint32_t n_tile
                                 uint32_t sample_count, uint32_t mode, rt_work_counts* out) {
     if (!c || !tiles || !out || mode > RT_COUNT_DEVICE) return RT_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    int st = sync_all(c);
+    if (st) return st;
     LaunchArgs a{};
     uint64_t n_out = 0;
-    int st = prepare_tiles(c, tiles, n_tiles, choose_k(c, tile_pixels(tiles, n_tiles)), &a, &n_out);
+    st = prepare_tiles(c, tiles, n_tiles, choose_k(c, tile_pixels(tiles, n_tiles)), &a, &n_out);
     if (st) return st;
     a.sample_begin = sample_begin;
     a.sample_count = sample_count;
@@ -746,7 +888,9 @@ extern "C" int rt_destroy(rt_ctx* c) {
 }
 
 // render_to_target_gpu (draw_scene.rs:17-47) on one device: spp/batch launches over the whole
-// frame; after each, the RGBA8 target is refreshed and the update hook runs.
+// frame; after each, the RGBA8 target is refreshed and the update hook runs.  Pipelined: batch
+// i + 1 is enqueued before batch i's frame is read back, converted and handed to the hook, so
+// the device never waits on the host and launch i + 1 fills launch i's drain tail.
 extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* cam,
                                    const rt_render_info* info, uint32_t spp, uint32_t batch, int device,
                                    uint8_t* target, rt_update_hook hook, void* user) {
@@ -756,12 +900,40 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
     int st = rt_create(scene, cam, info, nullptr, device, &c);
     if (st) return st;
     const rt_tile full{0, 0, info->width, info->height};
-    std::vector<float> rgba((size_t)info->width * info->height * 4);
-    for (uint32_t s = 0; s < spp; s += batch) {
-        st = rt_render(c, &full, 1, s, batch, rgba.data());
-        if (st) break;
-        rt_rgba_to_u8(rgba.data(), (uint64_t)info->width * info->height, target);
-        if (hook) hook(user, s + batch);
+    const uint64_t npix = (uint64_t)info->width * info->height;
+    std::vector<float> rgba(npix * 4);
+    float4* dbuf[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    auto run = [&]() -> int {
+        for (int k = 0; k < 2; ++k) {
+            if (hipMalloc(&dbuf[k], npix * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "output alloc failed");
+            HIPCHK(c, hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+        }
+        auto deliver = [&](uint32_t s_end, int k) -> int {
+            HIPCHK(c, hipEventSynchronize(done[k]));
+            HIPCHK(c, hipMemcpy(rgba.data(), dbuf[k], npix * sizeof(float4), hipMemcpyDeviceToHost));
+            rt_rgba_to_u8(rgba.data(), npix, target);
+            if (hook) hook(user, s_end);
+            return RT_OK;
+        };
+        uint32_t i = 0;
+        for (uint32_t s = 0; s < spp; s += batch, ++i) {
+            int r = render_impl(c, &full, 1, s, batch, dbuf[i % 2], nullptr);
+            if (r) return r;
+            HIPCHK(c, hipEventRecord(done[i % 2], c->slot[(c->next_slot + N_SLOTS - 1) % N_SLOTS].stream));
+            if (i > 0 && (r = deliver(s, (i - 1) % 2))) return r;
+        }
+        if (i > 0) return deliver(spp, (i - 1) % 2);
+        return RT_OK;
+    };
+    st = run();
+    if (!st) st = sync_all(c);
+    for (int k = 0; k < 2; ++k) {
+        if (done[k]) (void)hipEventDestroy(done[k]);
+        if (dbuf[k]) {
+            (void)sync_all(c);
+            (void)hipFree(dbuf[k]);
+        }
     }
     rt_destroy(c);
     return st;

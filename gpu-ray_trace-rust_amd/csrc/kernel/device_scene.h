@@ -15,6 +15,12 @@ constexpr int BLOCK_W = 16;
 constexpr int BLOCK_H = BLOCK / BLOCK_W;
 constexpr int MAX_STACK = 64;    // deepest KD tree the device path accepts (stack in LDS)
 
+// Leaf node (rt_kd_node {count, (offset << 2) | 3}) on the device: the low 24 bits of the first
+// word hold the ref count, the top 8 the number of sphere refs that open the leaf's list (refs
+// keep renderable order, where spheres usually precede every triangle; 0 when it does not fit).
+constexpr uint32_t LEAF_COUNT_MASK = (1u << 24) - 1u;
+constexpr uint32_t LEAF_LEAD_SHIFT = 24;
+
 // Device ref encoding: kind in the top 2 bits, index into the kind's arrays below.
 constexpr uint32_t REF_KIND_SHIFT = 30;
 constexpr uint32_t REF_INDEX_MASK = (1u << 30) - 1u;
@@ -69,6 +75,7 @@ struct DevScene {
     uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
     uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
     uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
+    uint32_t restart;       // queue kernels traverse stackless (kd-restart with push-down)
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r
@@ -76,7 +83,9 @@ struct DevScene {
     uint32_t n_spheres;
     // free triangles
     // Leaf-testable primitives, 3 float4 each, indexed by a device ref's index:
-    // [spheres: {c, r}, 0, 0][free triangles: v0, v1, v2][mesh triangles: v0, v1, v2].
+    // [spheres: {c, r}, 0, 0][free triangles: v0, e1, e2][mesh triangles: v0, e1, e2], with the
+    // Moller-Trumbore edges e1 = v1 - v0, e2 = v2 - v0 computed on the host by the same f32
+    // subtraction generic.rs:104-105 performs per test.
     // A ref's index is its pool position; per-kind arrays below take index - pool_<kind>.
     const float4* prim4;
     uint32_t pool_ftri, pool_mesh;

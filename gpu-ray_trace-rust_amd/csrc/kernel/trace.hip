@@ -248,11 +248,10 @@ __device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float* l) {
     return sphere_roots(sphere_disc(s, s.w * s.w, r), l);
 }
 
-// Triangle::intersect, Möller–Trumbore (triangle/generic.rs:102-137)
-__device__ __forceinline__ bool tri_hit(V3 v0, V3 v1, V3 v2, const Ray& r, float* l, float* bu,
+// Triangle::intersect, Möller–Trumbore (triangle/generic.rs:102-137), from the vertex v0 and
+// the edges e1 = v1 - v0, e2 = v2 - v0 the host computed (DevScene::prim4)
+__device__ __forceinline__ bool tri_hit(V3 v0, V3 e1, V3 e2, const Ray& r, float* l, float* bu,
                                         float* bv) {
-    V3 e1 = v1 - v0;
-    V3 e2 = v2 - v0;
     V3 ray_x_e2 = cross(r.d, e2);
     float det = dot(e1, ray_x_e2);
     if (fabsf(det) < EPS) return false;
@@ -469,15 +468,16 @@ __device__ __forceinline__ bool entry_exit(const float* b, const RayAx& ax, cons
 // The descent step is branch-free: the current branch is always written to slot sp (above the
 // stack top when nothing is pushed; a branch at depth D has sp <= D < stack_depth) and sp only
 // advances on a push, so the three reference cases (near / far / push both) are selects.
-template <bool COUNT, bool GEN, bool FAST, bool SMALL = false>
+template <bool COUNT, bool GEN, bool FAST, bool SMALL = false, bool RESTART = false>
 __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, const RayAx& ax,
                                              float root_entry, float root_exit, Hit* best, uint32_t* st,
                                              Ctr<COUNT>& c, uint32_t imin = 0, float lmin = 0.f) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
-    uint32_t node = 0;
+    uint32_t node = 0, restart = 0;
     int sp = 0;
     for (;;) {
         uint2 nd = fetch_node(sc, node);
+        bool pushed = false;
         while ((nd.y & 3u) != RT_KD_LEAF) {
             if (COUNT) c.nodes++;
             float d;
@@ -486,17 +486,30 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, c
             const bool go_near = t >= exit_t;   // kdtree.rs:80
             const bool go_far = !go_near && t <= entry;  // kdtree.rs:82
             const bool push = !go_near && !go_far;       // kdtree.rs:84-87
-            st[sp * BLOCK] = node;
-            sp += push ? 1 : 0;
-            top_t = push ? t : top_t;
+            if (!RESTART) {
+                st[sp * BLOCK] = node;
+                sp += push ? 1 : 0;
+                top_t = push ? t : top_t;
+            }
             exit_t = push ? t : exit_t;
             node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
+            if (RESTART) {  // stackless: see stack_search_coop
+                pushed = pushed || push;
+                restart = pushed ? restart : node;
+            }
             nd = fetch_node(sc, node);
         }
-        if (COUNT) { c.nodes++; c.leaf_refs += nd.x; }
-        if (leaf_closest<COUNT, GEN, SMALL>(sc, nd.y >> 2, nd.x, r, best, c, imin, lmin) &&
+        if (COUNT) { c.nodes++; c.leaf_refs += nd.x & LEAF_COUNT_MASK; }
+        if (leaf_closest<COUNT, GEN, SMALL>(sc, nd.y >> 2, nd.x & LEAF_COUNT_MASK, r, best, c, imin, lmin) &&
             best->l <= exit_t + EPS)
             return true;
+        if (RESTART) {
+            if (!pushed) return false;
+            entry = exit_t;
+            exit_t = root_exit;
+            node = restart;
+            continue;
+        }
         if (sp == 0) return false;
         --sp;
         const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
@@ -559,7 +572,7 @@ __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const Ray
 // and exit untouched — so the returned sphere and distance are the reference's.  Most rays
 // need no descent at all (in_return_leaf).  The instrumented kernel counts the reference's work with the plain traversal and the device's
 // work (count_device) through this function.
-template <bool COUNT>
+template <bool COUNT, bool RESTART = false>
 __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, Hit* best,
                                               uint32_t* st, Ctr<COUNT>& c) {
     uint32_t imin = 0;
@@ -604,9 +617,9 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
         bool found;
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, false, true, true>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
+            found = stack_search<COUNT, false, true, true, RESTART>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
         else
-            found = stack_search<COUNT, false, false, true>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
+            found = stack_search<COUNT, false, false, true, RESTART>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
         if (found) return true;
     }
     if (sc.has_cube) {
@@ -617,20 +630,20 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
     return false;
 }
 
-template <bool COUNT, bool GEN>
+template <bool COUNT, bool GEN, bool RESTART = false>
 __device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* best,
                                         uint32_t* st, Ctr<COUNT>& c) {
     if (!GEN && (!COUNT || sc.count_device) && sc.n_spheres <= 32u && sc.small_ok)
-        return closest_small<COUNT>(sc, r, best, st, c);
+        return closest_small<COUNT, RESTART>(sc, r, best, st, c);
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
         bool found;
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, GEN, true>(sc, r, ax, root_entry, root_exit, best, st, c);
+            found = stack_search<COUNT, GEN, true, false, RESTART>(sc, r, ax, root_entry, root_exit, best, st, c);
         else
-            found = stack_search<COUNT, GEN, false>(sc, r, ax, root_entry, root_exit, best, st, c);
+            found = stack_search<COUNT, GEN, false, false, RESTART>(sc, r, ax, root_entry, root_exit, best, st, c);
         if (found) return true;
     }
     // unconditional renderables: every cube map hits at +inf, the first one wins
@@ -653,8 +666,6 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* b
 // is the first strict minimum in leaf order (closest_hit.rs:25), exactly; NaN lengths never
 // win (see leaf_closest).  The owner then re-tests the winning ref for its barycentrics.
 __shared__ unsigned long long g_coop_key[BLOCK];
-__shared__ uint32_t g_coop_slot[BLOCK];
-
 
 // Inclusive prefix maximum over the 64 lanes (the DPP pattern of wave_incl_scan with max).
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
@@ -684,13 +695,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
 
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
 // Returns the lane's leaf minimum as (bits(l) << 32 | index into sc.refs), ~0 for none; one
-// leaf's refs are contiguous, so the index orders like the position in the leaf.
+// leaf's refs are contiguous, so the index orders like the position in the leaf.  `key0` is
+// the lane's minimum over refs it tested itself (the leaf's leading spheres).
 __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
-                                                        uint32_t cnt, uint32_t lane) {
+                                                        uint32_t cnt, uint32_t lane, unsigned long long key0) {
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
-    __hip_atomic_store(&g_coop_key[threadIdx.x], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_store(&g_coop_key[threadIdx.x], key0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t w = base + lane;
         uint32_t owner = 0;  // lanes whose inclusive end is <= w
@@ -705,12 +717,15 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
         if (w < total) {
+            // the primitive's three float4 are loaded before the kind is known (a sphere's are
+            // {c, r} and padding): one round trip to L2 after the ref, not two
             const uint32_t ref = sc.refs[idx];
             const float4* pd = prim_data(sc, ref);
+            const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
             float l = 0.f, bu, bv;
             bool h;
-            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(pd[0], ro, &l);
-            else h = tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), ro, &l, &bu, &bv);
+            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
+            else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
             if (h && l >= HIT_MIN)  // valid and not NaN
                 atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
         }
@@ -720,19 +735,31 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 
 // stack_search with cooperative leaves: the same per-lane traversal (kdtree.rs:66-104); lanes
 // whose search has ended (or that had no ray) keep looping as helpers until the wave is done.
-template <bool FAST>
+//
+// RESTART (stackless, kd-restart with push-down): no stack.  After a leaf that does not return,
+// the descent starts again with entry = that leaf's exit, from the deepest node the previous
+// descent reached before its first push (every node above it went near with the full interval
+// or far, and still does with the larger entry).  It reaches the reference's next leaf with the
+// same interval, bit for bit: the deepest push has t = the new entry exactly (the same quotient
+// of the same operands), so it now goes far — the reference's pop — while the shallower pushes,
+// whose t is strictly larger, go near again with exit = their t, as their stack entries would
+// have left it.  The remaining interval is empty exactly when the descent pushed nothing
+// (exit == root exit), the reference's empty stack.
+template <bool FAST, bool RESTART>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
                                                   uint32_t* st) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
-    uint32_t node = 0;
+    uint32_t node = 0, restart = 0;
     int sp = 0;
-    bool done = !active, found = false;
+    bool done = !active, found = false, pushed = false;
     const uint32_t lane = __lane_id();
     while (__ballot(!done) != 0) {
         uint32_t off = 0, cnt = 0;
+        unsigned long long key0 = ~0ull;
         if (!done) {
             uint2 nd = fetch_node(sc, node);
+            pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
                 float d;
                 const float t = split_t<FAST>(nd, ax, r, &d);
@@ -740,25 +767,42 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 const bool go_near = t >= exit_t;
                 const bool go_far = !go_near && t <= entry;
                 const bool push = !go_near && !go_far;
-                st[sp * BLOCK] = node;
-                sp += push ? 1 : 0;
-                top_t = push ? t : top_t;
+                if (!RESTART) {
+                    st[sp * BLOCK] = node;
+                    sp += push ? 1 : 0;
+                    top_t = push ? t : top_t;
+                }
                 exit_t = push ? t : exit_t;
                 node = (nd.y >> 2) + (go_far == pos ? 1u : 0u);
+                if (RESTART) {
+                    pushed = pushed || push;
+                    restart = pushed ? restart : node;
+                }
                 nd = fetch_node(sc, node);
             }
+            // The leaf's leading spheres (a scene's lights span most leaves) are this lane's own
+            // tests; the wave's passes then hold triangles only, with no sphere / triangle split.
             off = nd.y >> 2;
-            cnt = nd.x;
+            cnt = nd.x & LEAF_COUNT_MASK;
+            const uint32_t lead = nd.x >> LEAF_LEAD_SHIFT;
+            for (uint32_t j = 0; j < lead; ++j) {
+                float l;
+                if (sphere_hit(prim_data(sc, sc.refs[off + j])[0], r, &l) && l >= HIT_MIN)
+                    key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
+            }
+            off += lead;
+            cnt -= lead;
         }
-        const unsigned long long key = coop_leaf(sc, r, off, cnt, lane);
+        const unsigned long long key = coop_leaf(sc, r, off, cnt, lane, key0);
         if (!done) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
                 const uint32_t ref = sc.refs[(uint32_t)key];
                 const float4* pd = prim_data(sc, ref);
+                const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
                 float l = 0.f, bu = 0.f, bv = 0.f;
-                if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(pd[0], r, &l);
-                else (void)tri_hit(xyz(pd[0]), xyz(pd[1]), xyz(pd[2]), r, &l, &bu, &bv);
+                if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(a0, r, &l);
+                else (void)tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
                 best->ref = ref;
                 best->l = l;
                 best->bu = bu;
@@ -768,8 +812,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             if (ret) {
                 done = true;
                 found = true;
-            } else if (sp == 0) {
+            } else if (RESTART ? !pushed : sp == 0) {
                 done = true;
+            } else if (RESTART) {
+                entry = exit_t;
+                exit_t = root_exit;
+                node = restart;
             } else {
                 --sp;
                 const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
@@ -791,6 +839,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
 
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
+template <bool RESTART>
 __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
                                              uint32_t* st, bool active) {
     float root_entry = 0.f, root_exit = 0.f;
@@ -799,9 +848,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     bool found;
     const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
     if (__builtin_expect(__ballot(!fast) == 0, 1))
-        found = stack_search_coop<true>(sc, r, ax, in, root_entry, root_exit, best, st);
+        found = stack_search_coop<true, RESTART>(sc, r, ax, in, root_entry, root_exit, best, st);
     else
-        found = stack_search_coop<false>(sc, r, ax, in, root_entry, root_exit, best, st);
+        found = stack_search_coop<false, RESTART>(sc, r, ax, in, root_entry, root_exit, best, st);
     if (found) return true;
     if (active && sc.has_cube) {
         best->ref = REF_CUBE;
@@ -1127,7 +1176,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     return ++p.depth >= MAX_BOUNCES;
 }
 
-template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false>
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true) {
     if (COUNT) c.segments++;
@@ -1136,7 +1185,8 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop(sc, p.ray, &h, st, active) : closest<COUNT, GEN>(sc, p.ray, &h, st, c);
+    const bool hit = COOP ? closest_coop<RESTART>(sc, p.ray, &h, st, active)
+                          : closest<COUNT, GEN, RESTART>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
 }
@@ -1295,7 +1345,7 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
     return g < qmin ? qmin : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
-template <bool GEN, bool DLS = false>
+template <bool GEN, bool DLS, bool RESTART>
 __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
@@ -1356,8 +1406,8 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
-        const bool fin = GEN ? segment<false, GEN, DLS, GEN>(sc, p, st, c, have) && have
-                                          : have && segment<false, GEN, DLS>(sc, p, st, c);
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART>(sc, p, st, c, have) && have
+                             : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;
@@ -1431,29 +1481,39 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((trace_kernel<false, true>), dim3(a.n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
     return hipGetLastError();
 }
+
+// The queue kernel of a launch: sphere-only or general, with direct-light sampling, stackless or
+// with a traversal stack (DevScene::restart).  The stack is in LDS for the general kernels and in
+// global memory for the sphere-only one (queue_gstack_bytes); the stackless kernels need neither.
+template <class F>
+static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
+    const bool rs = a.sc.restart != 0;
+    if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
+    if (a.sc.spheres_only) return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
+    return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
+}
+static size_t queue_lds_bytes(const LaunchArgs& a, bool gen) {
+    return (gen && !a.sc.restart) ? stack_lds_bytes(a) : 0;
+}
+
 // Resident workgroups per CU of the queue kernel this scene launches (its registers and LDS
 // stack decide): the queue grid is exactly that many workgroups per CU.
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks) {
-    const size_t lds = stack_lds_bytes(a);
-    if (a.sc.dls) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true, true>, BLOCK, lds);
-    if (a.sc.spheres_only)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<false>, BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, queue_kernel<true>, BLOCK, lds);
+    return with_queue_kernel(a, [&](auto k, bool gen) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, BLOCK, queue_lds_bytes(a, gen));
+    });
 }
 
 size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks) {
-    if (!a.sc.spheres_only || a.sc.dls) return 0;
+    if (!a.sc.spheres_only || a.sc.dls || a.sc.restart) return 0;
     return (size_t)n_blocks * BLOCK * a.sc.stack_depth * sizeof(uint32_t);
 }
 
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
-    if (a.sc.dls)
-        hipLaunchKernelGGL((queue_kernel<true, true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
-    else if (a.sc.spheres_only)
-        hipLaunchKernelGGL((queue_kernel<false>), dim3(n_blocks), dim3(BLOCK), 0, s, a);
-    else
-        hipLaunchKernelGGL((queue_kernel<true>), dim3(n_blocks), dim3(BLOCK), stack_lds_bytes(a), s, a);
-    return hipGetLastError();
+    return with_queue_kernel(a, [&](auto k, bool gen) {
+        hipLaunchKernelGGL(k, dim3(n_blocks), dim3(BLOCK), queue_lds_bytes(a, gen), s, a);
+        return hipGetLastError();
+    });
 }
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s) {
     if (a.sc.dls)

@@ -139,6 +139,9 @@ EXPORTS = {
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32, P_f]),
     "rt_render_device": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
                                    C.c_void_p]),
+    "rt_render_device_async": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
+                                         C.c_void_p, C.c_void_p]),
+    "rt_synchronize": (C.c_int, [C.c_void_p]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P_f]),
     "rt_last_launch_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_launch_stats)]),
     "rt_count_work": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
@@ -180,12 +183,33 @@ def load_library(path: str | None = None):
         raise RuntimeError(f"{p} is missing: build the HIP extension first (__graft_entry__.build())")
     lib = C.CDLL(p)
     for name, (res, args) in EXPORTS.items():
+        if path is not None and not hasattr(lib, name):
+            continue  # an older build loaded for A/B (tools/variant_bench.py)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if path is None:
         _LIB = lib
     return lib
+
+
+def kernel_build_id(path: str | None = None) -> str:
+    """Identity of the library's device code: sha256 (16 hex digits) of its .hip_fatbin ELF
+    section.  Host-side changes leave it alone; any kernel change moves it.  Keys the committed
+    rocprofv3 counters (profiles/*_counters.json) to the build they were measured on."""
+    import hashlib
+    import struct
+
+    b = open(path or LIB_PATH, "rb").read()
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx][4]
+    for s in secs:
+        name = b[names + s[0]: b.index(b"\0", names + s[0])]
+        if name == b".hip_fatbin":
+            return hashlib.sha256(b[s[4]: s[4] + s[5]]).hexdigest()[:16]
+    raise RuntimeError("no .hip_fatbin section in " + (path or LIB_PATH))
 
 
 class RtError(RuntimeError):

@@ -109,6 +109,19 @@ class Context:
         abi.check(self.lib, self.lib.rt_render_device(self.ctx, arr, n, int(sample_begin), int(sample_count),
                                                       C.c_void_p(dev_ptr)), self.ctx)
 
+    def render_device_async(self, dev_ptr: int, tiles=None, sample_begin: int = 0, sample_count: int = 1,
+                            stream: int = 0):
+        """Enqueues the render and returns; `stream` is the caller's hipStream_t (0: the legacy
+        default stream, torch's default).  rt_synchronize / synchronize() waits for it."""
+        tiles = tiles or self.full_tile()
+        arr, n = tiles_array(tiles)
+        abi.check(self.lib, self.lib.rt_render_device_async(self.ctx, arr, n, int(sample_begin), int(sample_count),
+                                                            C.c_void_p(dev_ptr), C.c_void_p(stream or None)),
+                  self.ctx)
+
+    def synchronize(self):
+        abi.check(self.lib, self.lib.rt_synchronize(self.ctx), self.ctx)
+
     def last_kernel_ms(self) -> float:
         ms = C.c_float()
         abi.check(self.lib, self.lib.rt_last_kernel_ms(self.ctx, C.byref(ms)), self.ctx)

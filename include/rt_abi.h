@@ -240,13 +240,28 @@ int rt_create(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_
 int rt_render(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
               uint64_t sample_begin, uint32_t sample_count, float* out_rgba);
 
-/* Same, but the output goes to device memory on the ctx's device (for RCCL gathers);
- * returns once the kernel and the copy are complete. */
+/* Same, but the output goes to device memory on the ctx's device (for RCCL gathers); ordered
+ * after the work already enqueued on the legacy default stream (the caller's allocation of
+ * out_rgba_device, a gather still reading it), and complete on return. */
 int rt_render_device(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
                      uint64_t sample_begin, uint32_t sample_count, float* out_rgba_device);
 
-/* Device time (ms) of the last rt_render* call, first launch to last (trace + fold), from HIP
- * events. */
+/* Asynchronous rt_render_device: enqueues the call and returns.  `stream` is the caller's
+ * hipStream_t (NULL: the legacy default stream): what the caller enqueued on it before the call
+ * completes before the output is written, and what it enqueues after the call (a gather, a copy)
+ * sees the finished output.  Consecutive calls overlap on the device: call i + 1's trace starts
+ * while call i's last paths drain (draw_scene.rs:30-44's batches are independent sample ranges;
+ * only their running-mean folds are ordered).  Results equal the synchronous calls bit for bit.
+ * Stats (rt_last_launch_stats) cover every call since the previous rt_synchronize. */
+int rt_render_device_async(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
+                           uint64_t sample_begin, uint32_t sample_count, float* out_rgba_device,
+                           void* stream);
+
+/* Waits for every enqueued call of the ctx and closes its timing window. */
+int rt_synchronize(rt_ctx* ctx);
+
+/* Device time (ms) of the last synchronous rt_render* call (or of the async calls up to the
+ * last rt_synchronize), first trace launch to last fold, from HIP events. */
 int rt_last_kernel_ms(const rt_ctx* ctx, float* ms);
 
 /* Per-launch breakdown of the last rt_render* call: the trace kernel launches alone (HIP events

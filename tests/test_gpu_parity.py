@@ -360,3 +360,88 @@ def test_wide_frame_without_pixel_table(gpu_available, oracle):
     o1 = oracle.render(sc, [(34990, 0, 64, 3)], 0, 4, accum=oracle.ACCUM_FORWARD)
     assert np.array_equal(g, o), parity.stats(g, o)
     assert np.array_equal(g1, o1), parity.stats(g1, o1)
+
+
+@pytest.mark.parametrize("scene_name,spp,batch", [("walled", 12, 3), ("biplane", 6, 1), ("spaceship_r1", 6, 2)])
+def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, spp, batch):
+    """rt_render_device_async: consecutive batches overlap on two pipeline slots (trace i + 1
+    during trace i's drain; folds chained by events) == synchronous batches, bit for bit — also
+    with each batch split into several queue launches (small radiance cap) and with a
+    direct-schedule call in between."""
+    import torch
+
+    from rt_amd import render
+
+    sc = load_scene(scene_name)
+    w, h = sc.info.width, sc.info.height
+    tiles = [(w // 2 - 48, h // 2 - 24, 96, 48), (0, 0, 9, 5)]
+    n = 96 * 48 + 9 * 5
+    with render.Context(sc) as c1:
+        ref = c1.render(tiles, 0, spp)
+    for pipe, cap in (("1", None), ("0", None), ("1", str(3 * n * 2))):  # cap: 2 samples per launch
+        monkeypatch.setenv("RT_PIPELINE", pipe)  # overlapped launches, or each after the last fold
+        if cap:
+            monkeypatch.setenv("RT_QUEUE_RADIANCE_FLOATS", cap)
+        else:
+            monkeypatch.delenv("RT_QUEUE_RADIANCE_FLOATS", raising=False)
+        with render.Context(sc) as ca:
+            out = torch.full((n, 4), -1.0, dtype=torch.float32, device="cuda:0")
+            stream = torch.cuda.current_stream().cuda_stream
+            for s0 in range(0, spp, batch):
+                ca.render_device_async(out.data_ptr(), tiles, s0, batch, stream=stream)
+            got = out.cpu().numpy()  # ordered after the last fold on torch's stream
+            ca.synchronize()
+            st = ca.launch_stats()
+            assert st["n_trace_launches"] >= spp // batch
+        assert np.array_equal(got, ref), (pipe, cap, parity.stats(got, ref))
+    # a synchronous call between async ones
+    assert spp >= 3 * batch
+    monkeypatch.delenv("RT_QUEUE_RADIANCE_FLOATS", raising=False)
+    monkeypatch.delenv("RT_PIPELINE", raising=False)
+    with render.Context(sc) as cm:
+        out = torch.zeros((n, 4), dtype=torch.float32, device="cuda:0")
+        cm.render_device_async(out.data_ptr(), tiles, 0, batch)
+        mid = cm.render(tiles, batch, batch)  # synchronous
+        for s0 in range(2 * batch, spp, batch):
+            cm.render_device_async(out.data_ptr(), tiles, s0, batch)
+        cm.synchronize()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+    with render.Context(sc) as c2:
+        ref2 = c2.render(tiles, 0, 2 * batch)
+    assert np.array_equal(mid, ref2)
+    assert np.array_equal(got, ref)
+
+
+def test_render_to_target_pipelined_equals_batches(gpu_available):
+    """rt_render_to_target enqueues batch i + 1 before reading back batch i: every RGBA8 frame
+    handed to the update hook equals the synchronous batch loop's."""
+    from rt_amd import render
+
+    sc = load_scene("walled", width=160, height=96)
+    frames = []
+    render.render_to_target(sc, 6, 2, update_hook=lambda t, done: frames.append((done, t.copy())))
+    assert [d for d, _ in frames] == [2, 4, 6]
+    with render.Context(sc) as c:
+        for i, s0 in enumerate(range(0, 6, 2)):
+            img = c.render(None, s0, 2)
+            assert np.array_equal(frames[i][1].reshape(-1, 4), render.rgba_to_u8(img)), s0
+
+
+@pytest.mark.parametrize("scene_name,spp", [("walled", 9), ("triangles", 4), ("biplane", 3), ("spaceship_r1", 3),
+                                            ("a380", 2)])
+def test_stackless_traversal_bit_invariant(gpu_available, monkeypatch, scene_name, spp):
+    """Stackless kd-restart with push-down (RT_KD_RESTART=1: after a leaf, descend again from the
+    deepest node above the first push, entry = the leaf's exit) == the reference's stack
+    traversal (kdtree.rs:66-104), bit for bit, in the queue kernels."""
+    from rt_amd import render
+
+    sc = load_scene(scene_name)
+    w, h = sc.info.width, sc.info.height
+    tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
+    imgs = {}
+    for rs in ("0", "1"):
+        monkeypatch.setenv("RT_KD_RESTART", rs)
+        with render.Context(sc) as c:
+            imgs[rs] = c.render(tiles, 0, spp)
+    assert np.array_equal(imgs["0"], imgs["1"]), parity.stats(imgs["1"], imgs["0"])

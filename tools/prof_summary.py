@@ -22,6 +22,14 @@ def counters(path, kernels=("queue_kernel", "trace_kernel")):
     return per, names
 
 
+def bench_line(path):
+    if os.path.exists(path):
+        for l in open(path):
+            if l.startswith("{"):
+                return json.loads(l)
+    return {}
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles")
@@ -42,9 +50,9 @@ def main(tag):
             if l.startswith("{"):
                 d = json.loads(l)
                 lines += ["## bench.py line (under the profiler)", "", "```", l.strip(), "```", ""]
-    valu = {}
+    cnt = {}
     for part, title in (("fetch", "HBM read bytes (FETCH_SIZE, own pass)"), ("sq", "SQ counters (own pass)"),
-                        ("sq2", "SQ lane utilisation (own pass)")):
+                        ("sq2", "SQ lane utilisation (own pass)"), ("tcc", "L2 hits / misses (TCC, own pass)")):
         p = os.path.join(src, part, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -56,47 +64,42 @@ def main(tag):
         lines += [f"## {title}", "", "| dispatch | " + " | ".join(keys) + " |", "|---" * (len(keys) + 1) + "|"]
         for did, d in sorted(per.items(), key=lambda x: int(x[0])):
             lines.append(f"| {did} | " + " | ".join(f"{d[k]:.4g}" for k in keys) + " |")
-        d = list(per.values())[-1]
+        d = list(per.values())[-1]  # the last trace dispatch
+        cfg = bench_line(os.path.join(src, f"bench_{part}.log"))
+        if cfg:
+            cnt.setdefault("scene", cfg.get("metric", "").split(" on ")[-1].replace(".yml", ""))
+            cnt.setdefault("samples_per_launch", cfg.get("launch", {}).get("samples_per_launch", 0))
         if "FETCH_SIZE" in d:
+            cnt["hbm_read_bytes_per_launch"] = int(2 * d["FETCH_SIZE"] * 1024)
             lines.append(f"\nLast dispatch: FETCH_SIZE {d['FETCH_SIZE']:.1f} KB -> x2 (gfx950 correction) = "
                          f"{2 * d['FETCH_SIZE'] / 1024:.2f} MB read from HBM per launch.")
-            bl = os.path.join(src, "bench_fetch.log")
-            cfg = {}
-            if os.path.exists(bl):
-                for l in open(bl):
-                    if l.startswith("{"):
-                        cfg = json.loads(l)
-            scene = cfg.get("metric", "").split(" on ")[-1].replace(".yml", "") if cfg else None
-            spl = cfg.get("launch", {}).get("samples_per_launch", 0)
-            json.dump({"scene": scene, "samples_per_launch": spl,
-                       "hbm_read_bytes_per_launch": int(2 * d["FETCH_SIZE"] * 1024),
-                       "note": "rocprofv3 --pmc FETCH_SIZE, own pass, last trace dispatch, x2 per "
-                               "MI355X_MICROARCH.md HBM section"},
-                      open(os.path.join(dst, f"{tag}_fetch.json"), "w"), indent=1)
         if "SQ_INSTS_VALU" in d:
-            valu["valu_insts_per_launch"] = d["SQ_INSTS_VALU"]
+            cnt["valu_insts_per_launch"] = d["SQ_INSTS_VALU"]
         if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
-            valu["valu_lane_util"] = round(d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_ACTIVE_INST_VALU"]), 4)
+            cnt["valu_lane_util"] = round(d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_ACTIVE_INST_VALU"]), 4)
+            lines.append(f"\nLast dispatch: VALU lane utilisation = THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU) = "
+                         f"{cnt['valu_lane_util']:.1%}.")
         if "SQ_WAVE_CYCLES" in d:
             wc = d["SQ_WAVE_CYCLES"]
-            lines.append(f"\nLast dispatch: wait-any {d.get('SQ_WAIT_ANY', 0) / wc:.1%}, issuing {d.get('SQ_ACTIVE_INST_ANY', 0) / wc:.1%}, "
-                         f"issue-stall {d.get('SQ_WAIT_INST_ANY', 0) / wc:.1%} of wave cycles.")
-        if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
-            lines.append(f"\nLast dispatch: VALU lane utilisation = THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU) = "
-                         f"{d['SQ_THREAD_CYCLES_VALU'] / (64 * d['SQ_ACTIVE_INST_VALU']):.1%}.")
+            cnt["wait_any_frac"] = round(d.get("SQ_WAIT_ANY", 0) / wc, 4)
+            cnt["issue_frac"] = round(d.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4)
+            cnt["issue_stall_frac"] = round(d.get("SQ_WAIT_INST_ANY", 0) / wc, 4)
+            lines.append(f"\nLast dispatch: wait-any {cnt['wait_any_frac']:.1%}, issuing {cnt['issue_frac']:.1%}, "
+                         f"issue-stall {cnt['issue_stall_frac']:.1%} of wave cycles.")
+        if "TCC_HIT_sum" in d:
+            req = d["TCC_HIT_sum"] + d.get("TCC_MISS_sum", 0)
+            cnt["l2_bytes_per_launch"] = int(128 * req)
+            cnt["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(req, 1), 4)
+            lines.append(f"\nLast dispatch: L2 hit rate {cnt['l2_hit_rate']:.1%}, {req:.4g} requests "
+                         f"(x 128 B = {128 * req / 1e9:.3f} GB).")
         lines.append("")
-    if "valu_insts_per_launch" in valu:
-        bl = os.path.join(src, "bench_sq.log")
-        cfg = {}
-        if os.path.exists(bl):
-            for l in open(bl):
-                if l.startswith("{"):
-                    cfg = json.loads(l)
-        valu.update({"scene": cfg.get("metric", "").split(" on ")[-1].replace(".yml", "") if cfg else None,
-                     "samples_per_launch": cfg.get("launch", {}).get("samples_per_launch", 0),
-                     "note": "rocprofv3 --pmc SQ_INSTS_VALU (wave-level VALU instructions, all XCDs) and "
-                             "THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU), own passes, last trace dispatch"})
-        json.dump(valu, open(os.path.join(dst, f"{tag}_valu.json"), "w"), indent=1)
+    if cnt:
+        bid = os.path.join(src, "build_id")
+        cnt["build_id"] = open(bid).read().strip() if os.path.exists(bid) else None
+        cnt["note"] = ("rocprofv3 --pmc, one counter group per pass, last trace dispatch of the queue kernel; "
+                       "FETCH_SIZE x2 per MI355X_MICROARCH.md; build_id = rt_amd.abi.kernel_build_id() of the "
+                       "profiled library")
+        json.dump(cnt, open(os.path.join(dst, f"{tag}_counters.json"), "w"), indent=1)
     out = os.path.join(dst, f"{tag}_summary.md")
     open(out, "w").write("\n".join(lines) + "\n")
     print(open(out).read())

@@ -1,5 +1,6 @@
 """A/B timing of kernel variants in ONE process, interleaved rounds (cdna guide §5.4 rule 24).
-Usage: python tools/variant_bench.py [--scene walled] [--spp 32] [--rounds 3] name1 name2 ..."""
+Usage: python tools/variant_bench.py [--scene walled] [--spp 32] [--rounds 3] name1[:VAR=VAL,...] ...
+("main" is lib/librt_amd.so; other names lib/variants/librt_<name>.so)"""
 import argparse
 import json
 import os
@@ -23,9 +24,23 @@ def main():
     sch = scheme.load_json(os.path.join(ROOT, "tests", "golden", "scenes", a.scene + ".json"))
     ctxs = {}
     for n in a.names:
-        lib = abi.load_library(os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "variants", f"librt_{n}.so"))
+        # name[:VAR=VAL,...]: a library variant, with environment knobs read at its rt_create
+        lname, _, envs = n.partition(":")
+        saved = {}
+        for kv in filter(None, envs.split(",")):
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        path = (os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "librt_amd.so") if lname == "main" else
+                os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "variants", f"librt_{lname}.so"))
+        lib = abi.load_library(path)
         loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"), lib=lib)
         ctxs[n] = (render.Context(loaded, lib=lib), loaded)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     res = {n: [] for n in a.names}
     ref = None
     for r in range(a.rounds + 1):
