@@ -472,8 +472,13 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     // kd-restart with push-down, bit-identical (trace.hip stack_search_coop).  The stack is faster
     // on the mesh scenes; the sphere-only kernel, which descends for 0.05 nodes
     // per sample, runs stackless and needs no global stack.  RT_KD_RESTART=0/1 overrides.
+    // RT_KD_RESTART=2: stackless with the wave's leaf triangles staged in LDS per round (the
+    // general kernel; measured slower).
     d.restart = d.spheres_only ? 1u : 0u;
-    if (const char* e = std::getenv("RT_KD_RESTART")) d.restart = std::strcmp(e, "0") != 0 ? 1u : 0u;
+    if (const char* e = std::getenv("RT_KD_RESTART")) {
+        const unsigned long v = std::strtoul(e, nullptr, 10);
+        d.restart = v > 2 ? 1u : (uint32_t)v;
+    }
     // Overlapped launches pay off where the drain tail is long (mesh scenes: 8-10 ms per launch,
     // DESIGN.md §8); the sphere-only kernel's is ~0.4 ms.  RT_PIPELINE=0/1 overrides.
     c->overlap = !d.spheres_only;

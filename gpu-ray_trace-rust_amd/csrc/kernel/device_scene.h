@@ -75,7 +75,7 @@ struct DevScene {
     uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
     uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
     uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
-    uint32_t restart;       // queue kernels traverse stackless (kd-restart with push-down)
+    uint32_t restart;       // queue kernels: 0 stack, 1 stackless (kd-restart with push-down), 2 stackless + LDS triangle slabs
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

@@ -39,7 +39,10 @@
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 #endif
 #ifndef RT_MIN_WAVES_GEN
-#define RT_MIN_WAVES_GEN RT_MIN_WAVES  // the same for the general (triangle / mesh) kernels
+#define RT_MIN_WAVES_GEN 8  // general (triangle / mesh) kernels: 8 -> <=64 VGPRs; latency-bound, +2..7% over 7 (spills outside the pass loop)
+#endif
+#ifndef RT_SLAB_TRIS
+#define RT_SLAB_TRIS 96     // stackless general kernel: primitives per wave staged in LDS per round (0: none)
 #endif
 #ifndef RT_LDS_SPHERES
 #define RT_LDS_SPHERES 64   // 1 KiB
@@ -693,35 +696,106 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
     return v;
 }
 
+// Owner of item w of a wave-wide list: the number of lanes whose inclusive end (incl) is <= w.
+__device__ __forceinline__ uint32_t list_owner(uint32_t incl, uint32_t w) {
+    uint32_t owner = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t e = __shfl(incl, owner + step - 1);
+        owner += e <= w ? step : 0u;
+    }
+    return owner;
+}
+
+// Triangle slabs staged in LDS (the stackless general kernel, whose LDS holds no stack): per
+// round, the distinct leaves of the wave's lanes are copied once into the wave's slab (up to
+// RT_SLAB_TRIS primitives; leaves beyond it keep the global path), as {p0, p1 | ref, p2} with
+// p = the primitive's three pool float4 (DevScene::prim4) and the ref in p1.w.  Rays of one wave
+// start on neighbouring pixels, so most lanes share their leaf: a pair then reads its primitive
+// from LDS instead of a ref and three gathers from L1 / L2 per (ray, primitive) pair.
+__shared__ float4 g_slab[BLOCK / 64][RT_SLAB_TRIS > 0 ? 3 * RT_SLAB_TRIS : 1];
+constexpr uint32_t SLAB_NONE = 0x80000000u;  // a lane's slab delta when its leaf is not staged
+
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
 // Returns the lane's leaf minimum as (bits(l) << 32 | index into sc.refs), ~0 for none; one
 // leaf's refs are contiguous, so the index orders like the position in the leaf.  `key0` is
 // the lane's minimum over refs it tested itself (the leaf's leading spheres).
+template <bool SLAB>
 __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
                                                         uint32_t cnt, uint32_t lane, unsigned long long key0) {
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
     __hip_atomic_store(&g_coop_key[threadIdx.x], key0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    // slab index of item w of this lane's leaf = w + sdelta (SLAB_NONE: not staged); valid
+    // deltas lie in (-2^31, RT_SLAB_TRIS), so the sentinel never collides
+    uint32_t sdelta = SLAB_NONE;
+    if constexpr (SLAB) {
+        float4* slab = g_slab[threadIdx.x >> 6];
+        // lanes grouped by leaf (equal offsets: equal ref lists), groups in lane order of their
+        // first lane, staged while they fit
+        uint64_t pending = __ballot(cnt > 0);
+        uint32_t used = 0, lead_n = 0, sbase = 0;
+        bool staged = false;
+        while (pending) {
+            const uint32_t ld = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
+            const uint32_t o = __builtin_amdgcn_readlane(off, ld), n = __builtin_amdgcn_readlane(cnt, ld);
+            const uint64_t same = __ballot(off == o) & pending;
+            pending &= ~same;
+            if (used + n <= (uint32_t)RT_SLAB_TRIS) {
+                if ((same >> lane) & 1ull) { staged = true; sbase = used; }
+                if (lane == ld) lead_n = n;
+                used += n;
+            }
+        }
+        if (used) {
+            // the staged lists, concatenated, copied by the whole wave (a pass of the same shape
+            // as the test passes below)
+            const uint32_t fincl = wave_incl_scan(lead_n, lane);
+            for (uint32_t fb = 0; fb < used; fb += 64) {
+                const uint32_t w = fb + lane;
+                const uint32_t fo = list_owner(fincl, w);
+                const uint32_t src = w + __shfl(off - (fincl - lead_n), fo);
+                if (w < used) {
+                    const uint32_t ref = sc.refs[src];
+                    const float4* pd = prim_data(sc, ref);
+                    const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
+                    slab[3 * w] = a0;
+                    slab[3 * w + 1] = make_float4(a1.x, a1.y, a1.z, __uint_as_float(ref));
+                    slab[3 * w + 2] = a2;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the slab's writes before any lane's reads
+        }
+        if (staged) sdelta = sbase - (incl - cnt);
+    }
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t w = base + lane;
-        uint32_t owner = 0;  // lanes whose inclusive end is <= w
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-            const uint32_t e = __shfl(incl, owner + step - 1);
-            owner += e <= w ? step : 0u;
-        }
+        const uint32_t owner = list_owner(incl, w);
         // item w of the owner's leaf is sc.refs[w + (off - start)] of the owner: one shuffle
         const uint32_t idx = w + __shfl(off - (incl - cnt), owner);
+        const uint32_t od = SLAB ? __shfl(sdelta, owner) : SLAB_NONE;
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
         if (w < total) {
-            // the primitive's three float4 are loaded before the kind is known (a sphere's are
-            // {c, r} and padding): one round trip to L2 after the ref, not two
-            const uint32_t ref = sc.refs[idx];
-            const float4* pd = prim_data(sc, ref);
-            const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
+            uint32_t ref;
+            float4 a0, a1, a2;
+            if (SLAB && od != SLAB_NONE) {
+                const float4* sp = g_slab[threadIdx.x >> 6] + 3 * (w + od);
+                a0 = sp[0];
+                a1 = sp[1];
+                a2 = sp[2];
+                ref = __float_as_uint(a1.w);
+            } else {
+                // the primitive's three float4 are loaded before the kind is known (a sphere's
+                // are {c, r} and padding): one round trip to L2 after the ref, not two
+                ref = sc.refs[idx];
+                const float4* pd = prim_data(sc, ref);
+                a0 = pd[0];
+                a1 = pd[1];
+                a2 = pd[2];
+            }
             float l = 0.f, bu, bv;
             bool h;
             if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
@@ -730,6 +804,7 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
         }
     }
+    if (SLAB) __builtin_amdgcn_wave_barrier();  // every read of this round's slab before the next fill
     return __hip_atomic_load(&g_coop_key[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
@@ -745,7 +820,7 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
-template <bool FAST, bool RESTART>
+template <bool FAST, bool RESTART, bool SLAB>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
                                                   uint32_t* st) {
@@ -793,7 +868,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             off += lead;
             cnt -= lead;
         }
-        const unsigned long long key = coop_leaf(sc, r, off, cnt, lane, key0);
+        const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
         if (!done) {
             bool ret = false;
             if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
@@ -839,7 +914,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
 
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
-template <bool RESTART>
+template <bool RESTART, bool SLAB>
 __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
                                              uint32_t* st, bool active) {
     float root_entry = 0.f, root_exit = 0.f;
@@ -848,9 +923,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     bool found;
     const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
     if (__builtin_expect(__ballot(!fast) == 0, 1))
-        found = stack_search_coop<true, RESTART>(sc, r, ax, in, root_entry, root_exit, best, st);
+        found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in, root_entry, root_exit, best, st);
     else
-        found = stack_search_coop<false, RESTART>(sc, r, ax, in, root_entry, root_exit, best, st);
+        found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in, root_entry, root_exit, best, st);
     if (found) return true;
     if (active && sc.has_cube) {
         best->ref = REF_CUBE;
@@ -1176,7 +1251,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     return ++p.depth >= MAX_BOUNCES;
 }
 
-template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false>
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool SLAB = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true) {
     if (COUNT) c.segments++;
@@ -1185,7 +1260,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop<RESTART>(sc, p.ray, &h, st, active)
+    const bool hit = COOP ? closest_coop<RESTART, SLAB>(sc, p.ray, &h, st, active)
                           : closest<COUNT, GEN, RESTART>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
@@ -1345,7 +1420,7 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
     return g < qmin ? qmin : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
-template <bool GEN, bool DLS, bool RESTART>
+template <bool GEN, bool DLS, bool RESTART, bool SLAB = false>
 __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
@@ -1406,7 +1481,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
-        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART>(sc, p, st, c, have) && have
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
@@ -1483,13 +1558,15 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
 }
 
 // The queue kernel of a launch: sphere-only or general, with direct-light sampling, stackless or
-// with a traversal stack (DevScene::restart).  The stack is in LDS for the general kernels and in
-// global memory for the sphere-only one (queue_gstack_bytes); the stackless kernels need neither.
+// with a traversal stack (DevScene::restart: 0 stack, 1 stackless, 2 stackless with the triangle
+// slabs of coop_leaf).  The stack is in LDS for the general kernels and in global memory for the
+// sphere-only one (queue_gstack_bytes); the stackless kernels need neither.
 template <class F>
 static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
-    const bool rs = a.sc.restart != 0;
+    const uint32_t rs = a.sc.restart;
     if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
     if (a.sc.spheres_only) return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
+    if (rs == 2) return f(queue_kernel<true, false, true, true>, true);
     return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
 }
 static size_t queue_lds_bytes(const LaunchArgs& a, bool gen) {

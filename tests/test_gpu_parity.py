@@ -440,8 +440,9 @@ def test_stackless_traversal_bit_invariant(gpu_available, monkeypatch, scene_nam
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
     imgs = {}
-    for rs in ("0", "1"):
+    for rs in ("0", "1", "2"):  # 2: stackless with the leaves' triangles staged in LDS
         monkeypatch.setenv("RT_KD_RESTART", rs)
         with render.Context(sc) as c:
             imgs[rs] = c.render(tiles, 0, spp)
     assert np.array_equal(imgs["0"], imgs["1"]), parity.stats(imgs["1"], imgs["0"])
+    assert np.array_equal(imgs["0"], imgs["2"]), parity.stats(imgs["2"], imgs["0"])
