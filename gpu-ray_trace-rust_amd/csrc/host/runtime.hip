@@ -31,11 +31,16 @@ using namespace rth;
 // (4 GiB cap).  RT_QUEUE_RADIANCE_GIB overrides it; only what a launch needs is allocated.
 static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 
-// The queue launches alternate between two pipeline slots, each with its own stream, radiance
+// Overlapped queue launches rotate over pipeline slots, each with its own stream, radiance
 // buffer, item counter and traversal-stack scratch: launch i + 1 starts while launch i drains
 // (its last paths finish on a few lanes), and only the folds, which update the shared
-// accumulators and the output, are chained in order by events.
-constexpr int N_SLOTS = 2;
+// accumulators and the output, are chained in order by events.  A mesh launch's drain tail is
+// ~8-10 ms; a 1-spp a380 launch holds ~3 ms of work, so small launches need more of them in
+// flight to cover one tail: 3 slots for launches of up to 2^21 samples, else 2 (A/B over 2, 3
+// and 4 slots: a380 at 1 spp 143 / 189 / 164 Msamples/s; biplane at 10 spp 508 / 507 / 436;
+// spaceship at 25 spp 267 / 258 / 256).  RT_PIPELINE_SLOTS (2-4) fixes the count.
+constexpr int N_SLOTS = 4;
+constexpr uint64_t SMALL_LAUNCH_ITEMS = 1ull << 21;
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t fold_done = nullptr;   // this slot's last fold (its radiance buffer is free again)
@@ -50,7 +55,7 @@ struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;     // = slot[0].stream: uploads, synchronous paths
     Slot slot[N_SLOTS];
-    uint32_t next_slot = 0;
+    uint32_t cur_slot = 0;            // the slot of the last enqueued launch
     hipEvent_t last_fold = nullptr;   // the most recent fold enqueued (nullptr: none pending)
     hipEvent_t caller_ev = nullptr;   // the caller's stream, recorded at an async call
     // Timing window: every trace launch since the window opened, as start / stop event pairs,
@@ -79,6 +84,8 @@ struct rt_ctx {
     int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
     uint64_t queue_floats = 0;    // RT_QUEUE_RADIANCE_GIB: radiance buffer cap per queue launch
     bool overlap = true;          // RT_PIPELINE: launch i + 1 may start during launch i's drain
+    uint64_t overlap_max_items = 1ull << 27;  // ... when it has at most this many samples
+    uint32_t n_slots = 0;         // RT_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
     float last_ms = 0.f;
     std::string err;
 };
@@ -482,7 +489,14 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     // Overlapped launches pay off where the drain tail is long (mesh scenes: 8-10 ms per launch,
     // DESIGN.md §8); the sphere-only kernel's is ~0.4 ms.  RT_PIPELINE=0/1 overrides.
     c->overlap = !d.spheres_only;
-    if (const char* e = std::getenv("RT_PIPELINE")) c->overlap = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("RT_PIPELINE_SLOTS")) {
+        const unsigned long v = std::strtoul(e, nullptr, 10);
+        if (v >= 2 && v <= (unsigned long)N_SLOTS) c->n_slots = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("RT_PIPELINE")) {  // 0: never, 1: below the item limit, 2: always
+        c->overlap = std::strcmp(e, "0") != 0;
+        if (!std::strcmp(e, "2")) c->overlap_max_items = ~0ull;
+    }
     if (const char* e = std::getenv("RT_QUEUE_RADIANCE_FLOATS")) {  // tests: force split launches
         unsigned long long v = std::strtoull(e, nullptr, 10);
         if (v >= 3 && v <= (1ull << 34)) c->queue_floats = (uint64_t)v;
@@ -680,12 +694,24 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
     }
     uint32_t done = 0;
     do {
-        Slot& sl = c->slot[c->next_slot];
-        c->next_slot = (c->next_slot + 1) % N_SLOTS;
         a.sample_begin = sample_begin + done;
         a.sample_count = (uint32_t)(sample_count - done < chunk ? sample_count - done : chunk);
         a.n_items = (uint32_t)(n_out * a.sample_count);
-        int st = ensure_radiance(c, sl, 3 * n_out * (a.sample_count ? a.sample_count : 1));
+        // Without overlap the trace waits for the previous fold: the sphere-only kernel's drain
+        // tail is ~0.4 ms, and a fold beside the next persistent trace grid cost walled 2% (its
+        // workgroups take slots from that grid).  Mesh launches overlap while the ~10 ms tail is
+        // a sizeable share of the launch: up to overlap_max_items samples (a380 at 7.2 M: +19%,
+        // spaceship at 18 M: +10%; spaceship 4096^2 at 419 M: -2%, triangles at 720 M: -4%).
+        // Overlapped launches alternate slots; a serialized one stays on the last slot's stream,
+        // behind its fold, with one radiance buffer.
+        const bool overlap = c->overlap && a.n_items <= c->overlap_max_items;
+        const uint32_t n_slots = c->n_slots ? c->n_slots : (a.n_items <= SMALL_LAUNCH_ITEMS ? 3u : 2u);
+        if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
+        Slot& sl = c->slot[c->cur_slot];
+        const uint64_t floats = 3 * n_out * (a.sample_count ? a.sample_count : 1);
+        int st = ensure_radiance(c, sl, floats);
+        // every slot's buffer at once, so that no allocation lands between overlapped launches
+        for (uint32_t k = 0; overlap && !st && k < n_slots; ++k) st = ensure_radiance(c, c->slot[k], floats);
         if (st) return st;
         a.radiance = sl.radiance;
         a.queue = sl.queue;
@@ -701,10 +727,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
             }
             a.gstack = sl.gstack;
         }
-        // Without overlap the trace also waits for the previous fold: the sphere-only kernel's
-        // drain tail is ~0.4 ms, and a fold beside the next persistent trace grid cost walled 2%
-        // (its workgroups take slots from that grid).
-        if (!c->overlap && c->last_fold && c->last_fold != sl.fold_done)
+        if (!overlap && c->last_fold && c->last_fold != sl.fold_done)
             HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));
         if (a.sample_count) {
             HIPCHK(c, hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), sl.stream));
@@ -720,7 +743,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         done += a.sample_count;
     } while (done < sample_count);
     // the window ends at this fold (fold_done carries no timestamp)
-    HIPCHK(c, hipEventRecord(c->win_end_ev, c->slot[(c->next_slot + N_SLOTS - 1) % N_SLOTS].stream));
+    HIPCHK(c, hipEventRecord(c->win_end_ev, c->slot[c->cur_slot].stream));
     c->win_end = c->win_end_ev;
     return RT_OK;
 }
@@ -757,7 +780,7 @@ static int run_direct(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint32_t K, uint6
     }
     HIPCHK(c, hipEventRecord(sl.fold_done, sl.stream));
     c->last_fold = sl.fold_done;
-    c->next_slot = 1 % N_SLOTS;
+    c->cur_slot = 0;
     return RT_OK;
 }
 
@@ -798,7 +821,7 @@ extern "C" int rt_render(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
     if ((st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, out_rgba ? c->d_out : nullptr, nullptr))) return st;
     if (out_rgba)  // on the stream of the last fold
         HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost,
-                                 c->slot[(c->next_slot + N_SLOTS - 1) % N_SLOTS].stream));
+                                 c->slot[c->cur_slot].stream));
     return sync_all(c);
 }
 
@@ -925,7 +948,7 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
         for (uint32_t s = 0; s < spp; s += batch, ++i) {
             int r = render_impl(c, &full, 1, s, batch, dbuf[i % 2], nullptr);
             if (r) return r;
-            HIPCHK(c, hipEventRecord(done[i % 2], c->slot[(c->next_slot + N_SLOTS - 1) % N_SLOTS].stream));
+            HIPCHK(c, hipEventRecord(done[i % 2], c->slot[c->cur_slot].stream));
             if (i > 0 && (r = deliver(s, (i - 1) % 2))) return r;
         }
         if (i > 0) return deliver(spp, (i - 1) % 2);

@@ -378,7 +378,7 @@ def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, sp
     n = 96 * 48 + 9 * 5
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, spp)
-    for pipe, cap in (("1", None), ("0", None), ("1", str(3 * n * 2))):  # cap: 2 samples per launch
+    for pipe, cap in (("2", None), ("0", None), ("2", str(3 * n * 2))):  # cap: 2 samples per launch
         monkeypatch.setenv("RT_PIPELINE", pipe)  # overlapped launches, or each after the last fold
         if cap:
             monkeypatch.setenv("RT_QUEUE_RADIANCE_FLOATS", cap)
