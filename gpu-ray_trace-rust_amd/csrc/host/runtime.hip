@@ -73,6 +73,7 @@ struct rt_ctx {
     DevTile* d_tiles = nullptr;
     uint32_t d_tiles_cap = 0;
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
+    uint2* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
     float4* d_out = nullptr;
@@ -104,14 +105,21 @@ static int set_err(rt_ctx* c, int code, const std::string& msg) {
     return code;
 }
 
+#ifndef RT_PIX_BLOCK
+#define RT_PIX_BLOCK 8  // queue order of a launch's pixels: B x B blocks of each tile (1: row order)
+#endif
+
 template <class T>
 static int upload(rt_ctx* c, const std::vector<T>& v, const T** out) {
     *out = nullptr;
     if (v.empty()) return RT_OK;
     void* p = nullptr;
-    if (hipMalloc(&p, v.size() * sizeof(T)) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
+    // 64 zero bytes past the end: the packet traversal's scalar loads read refs eight at a time
+    constexpr size_t PAD = 64;
+    if (hipMalloc(&p, v.size() * sizeof(T) + PAD) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
     c->allocs.push_back(p);
     HIPCHK(c, hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(static_cast<char*>(p) + v.size() * sizeof(T), 0, PAD));
     *out = static_cast<const T*>(p);
     return RT_OK;
 }
@@ -157,6 +165,7 @@ static void destroy_ctx(rt_ctx* c) {
     if (c->accum) (void)hipFree(c->accum);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     if (c->d_pixmap) (void)hipFree(c->d_pixmap);
+    if (c->d_pixq) (void)hipFree(c->d_pixq);
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_counts) (void)hipFree(c->d_counts);
     for (Slot& sl : c->slot) {
@@ -382,6 +391,19 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
             pool[3 * t + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.f);
         }
         if ((st = upload(c, pool, &d.prim4))) return st;
+        std::vector<float4> pool8(2 * (pool.size() / 3));
+        for (size_t t = 0; t < pool.size() / 3; ++t) {
+            const float4 v0 = pool[3 * t], e1 = pool[3 * t + 1], e2 = pool[3 * t + 2];
+            pool8[2 * t] = t < scene->n_spheres ? v0 : make_float4(v0.x, v0.y, v0.z, e1.x);
+            pool8[2 * t + 1] = t < scene->n_spheres ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(e1.y, e1.z, e2.x, e2.y);
+        }
+        std::vector<float> zref(refs.size());
+        for (size_t i = 0; i < refs.size(); ++i) {
+            const size_t t = refs[i] & REF_INDEX_MASK;
+            zref[i] = t < scene->n_spheres ? 0.f : pool[3 * t + 2].z;
+        }
+        if ((st = upload(c, pool8, &d.prim8))) return st;
+        if ((st = upload(c, zref, &d.zref))) return st;
         d.pool_ftri = scene->n_spheres;
         d.pool_mesh = scene->n_spheres + scene->n_free_tris;
     }
@@ -606,18 +628,36 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
             for (const DevTile& d : dt)
                 for (uint32_t y = 0; y < d.h; ++y)
                     for (uint32_t x = 0; x < d.w; ++x) pm[d.out_off + (size_t)y * d.w + x] = ((d.y0 + y) << 16) | (d.x0 + x);
+            // queue order: RT_PIX_BLOCK x RT_PIX_BLOCK blocks of each tile, row by row
+            std::vector<uint2> pq;
+            pq.reserve(pix);
+            constexpr uint32_t B = RT_PIX_BLOCK > 0 ? RT_PIX_BLOCK : 1;
+            for (const DevTile& d : dt)
+                for (uint32_t by = 0; by < d.h; by += B)
+                    for (uint32_t bx = 0; bx < d.w; bx += B)
+                        for (uint32_t y = by; y < std::min(by + B, d.h); ++y)
+                            for (uint32_t x = bx; x < std::min(bx + B, d.w); ++x) {
+                                const uint32_t o = d.out_off + y * d.w + x;
+                                pq.push_back(make_uint2(pm[o], o));
+                            }
             if (pix > c->d_pixmap_cap) {
                 if (c->d_pixmap) (void)hipFree(c->d_pixmap);
+                if (c->d_pixq) (void)hipFree(c->d_pixq);
                 c->d_pixmap = nullptr;
+                c->d_pixq = nullptr;
                 c->d_pixmap_cap = 0;
-                if (hipMalloc(&c->d_pixmap, pix * sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "pixel map alloc failed");
+                if (hipMalloc(&c->d_pixmap, pix * sizeof(uint32_t)) != hipSuccess ||
+                    hipMalloc(&c->d_pixq, pix * sizeof(uint2)) != hipSuccess)
+                    return set_err(c, RT_ERR_OOM, "pixel map alloc failed");
                 c->d_pixmap_cap = pix;
             }
             HIPCHK(c, hipMemcpy(c->d_pixmap, pm.data(), pix * sizeof(uint32_t), hipMemcpyHostToDevice));
+            HIPCHK(c, hipMemcpy(c->d_pixq, pq.data(), pix * sizeof(uint2), hipMemcpyHostToDevice));
         }
         c->pixmap_tiles = dt;
     }
     a->pix_xy = (c->sc.width <= 65535u && c->sc.height <= 65535u) ? c->d_pixmap : nullptr;
+    a->pix_q = (a->pix_xy && RT_PIX_BLOCK > 1) ? c->d_pixq : nullptr;
     a->sc = c->sc;
     a->tiles = c->d_tiles;
     a->n_tiles = n_tiles;

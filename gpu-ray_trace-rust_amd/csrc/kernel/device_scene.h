@@ -88,6 +88,10 @@ struct DevScene {
     // subtraction generic.rs:104-105 performs per test.
     // A ref's index is its pool position; per-kind arrays below take index - pool_<kind>.
     const float4* prim4;
+    // RT_ZREF: the pool as two float4 per primitive, {v0, e1.x}, {e1.y, e1.z, e2.x, e2.y} (a
+    // sphere: {c, r}, 0), and e2.z in an array parallel to refs (zref[i] of refs[i])
+    const float4* prim8;
+    const float* zref;
     uint32_t pool_ftri, pool_mesh;
     // direct-light sampling (dir_light_samp): renderables in renderable order (device refs) and
     // the emissive spheres {sphere index, position in elem_refs}
@@ -137,6 +141,11 @@ struct LaunchArgs {
     const DevTile* tiles;
     uint32_t n_tiles;
     const uint32_t* pix_xy; // launch pixel o -> (y << 16) | x; nullptr for frames over 65535 wide/high
+    // Queue order of the launch pixels (with pix_xy): the queue kernel's q-th pixel of a sample
+    // is {(y << 16) | x, o}, 8 x 8 blocks of each tile in turn, so a wave's consecutive items
+    // are a compact block of the frame (coherent camera rays for closest_packet).  nullptr:
+    // q = o.
+    const uint2* pix_q;
     uint32_t n_blocks;
     uint64_t sample_begin;
     uint32_t sample_count;

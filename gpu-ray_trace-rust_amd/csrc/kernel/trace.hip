@@ -33,7 +33,7 @@
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 #endif
 #ifndef RT_REGEN_MIN_GEN
-#define RT_REGEN_MIN_GEN 1  // the same for the general queue kernel (16-40: no gain on the mesh scenes)
+#define RT_REGEN_MIN_GEN 16 // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
 #endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
@@ -43,6 +43,18 @@
 #endif
 #ifndef RT_SLAB_TRIS
 #define RT_SLAB_TRIS 96     // stackless general kernel: primitives per wave staged in LDS per round (0: none)
+#endif
+#ifndef RT_OWNER_LOOP
+#define RT_OWNER_LOOP 8     // cooperative pass: owners of a pass found by a readlane loop when at most this many leaves end in it (0: binary search)
+#endif
+#ifndef RT_PIPE_REF
+#define RT_PIPE_REF 0       // cooperative pass: the next pass's owners and refs loaded before this pass's test
+#endif
+#ifndef RT_PACKET
+#define RT_PACKET 1         // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
+#endif
+#ifndef RT_PACKET_MIN
+#define RT_PACKET_MIN 40    // fewest camera rays of one direction octant that form a packet
 #endif
 #ifndef RT_LDS_SPHERES
 #define RT_LDS_SPHERES 64   // 1 KiB
@@ -707,6 +719,26 @@ __device__ __forceinline__ uint32_t list_owner(uint32_t incl, uint32_t w) {
     return owner;
 }
 
+// Owner of item w (= base + lane) of a pass.  owner(w) = #lanes with incl <= w: lanes below o_lo
+// end at or before the pass's first item and lanes from o_hi on after its last one (incl is
+// non-decreasing), so when few leaves end inside the pass only the lanes in between are compared,
+// by readlane (scalar operands, no LDS round trip); otherwise the binary search of list_owner.
+// Every lane of the wave calls this with the same base.
+__device__ __forceinline__ uint32_t pass_owner(uint32_t incl, uint32_t total, uint32_t base, uint32_t w) {
+    if (RT_OWNER_LOOP > 0) {
+        const uint32_t last = min(base + 63u, total - 1u);
+        const uint32_t o_lo = (uint32_t)__popcll(__ballot(incl <= base));
+        const uint32_t o_hi = (uint32_t)__popcll(__ballot(incl <= last));
+        if (o_hi - o_lo <= (uint32_t)RT_OWNER_LOOP) {
+            uint32_t owner = o_lo;
+            for (uint32_t k = o_lo; k < o_hi; ++k)
+                owner += w >= (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)k) ? 1u : 0u;
+            return owner;
+        }
+    }
+    return list_owner(incl, w);
+}
+
 // Triangle slabs staged in LDS (the stackless general kernel, whose LDS holds no stack): per
 // round, the distinct leaves of the wave's lanes are copied once into the wave's slab (up to
 // RT_SLAB_TRIS primitives; leaves beyond it keep the global path), as {p0, p1 | ref, p2} with
@@ -769,18 +801,27 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
         }
         if (staged) sdelta = sbase - (incl - cnt);
     }
+    // item w of a lane's leaf is sc.refs[w + delta]
+    const uint32_t delta = off - (incl - cnt);
+    constexpr bool PIPE = RT_PIPE_REF && !SLAB;
+    uint32_t owner = 0, idx = 0, ref = 0;
+    if (PIPE && total) {
+        owner = pass_owner(incl, total, 0u, lane);
+        idx = lane + __shfl(delta, owner);
+        if (lane < total) ref = sc.refs[idx];
+    }
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t w = base + lane;
-        const uint32_t owner = list_owner(incl, w);
-        // item w of the owner's leaf is sc.refs[w + (off - start)] of the owner: one shuffle
-        const uint32_t idx = w + __shfl(off - (incl - cnt), owner);
-        const uint32_t od = SLAB ? __shfl(sdelta, owner) : SLAB_NONE;
+        if (!PIPE) {
+            owner = pass_owner(incl, total, base, w);
+            idx = w + __shfl(delta, owner);
+        }
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+        const uint32_t od = SLAB ? __shfl(sdelta, owner) : SLAB_NONE;
+        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
         if (w < total) {
-            uint32_t ref;
-            float4 a0, a1, a2;
             if (SLAB && od != SLAB_NONE) {
                 const float4* sp = g_slab[threadIdx.x >> 6] + 3 * (w + od);
                 a0 = sp[0];
@@ -790,18 +831,42 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             } else {
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
-                ref = sc.refs[idx];
+                if (!PIPE) ref = sc.refs[idx];
+#if defined(RT_PROBE_NOREF)
+                ref = (K_MESH_TRI << REF_KIND_SHIFT) | (sc.pool_mesh + (idx & 1023u));
+#endif
+#if defined(RT_ZREF)
+                const float4* q = sc.prim8 + 2 * (size_t)(ref & REF_INDEX_MASK);
+                const float4 b0 = q[0], b1 = q[1];
+                a0 = b0;
+                a1 = make_float4(b0.w, b1.x, b1.y, 0.f);
+                a2 = make_float4(b1.z, b1.w, sc.zref[idx], 0.f);
+#else
                 const float4* pd = prim_data(sc, ref);
                 a0 = pd[0];
                 a1 = pd[1];
+#if defined(RT_PROBE_NOA2)
+                a2 = a1;
+#else
                 a2 = pd[2];
+#endif
+#endif
             }
+        }
+        const uint32_t cur_owner = owner, cur_idx = idx, cur_ref = ref;
+        if (PIPE && base + 64u < total) {  // the next pass's owners and refs, in flight during this test
+            const uint32_t nb = base + 64u;
+            owner = pass_owner(incl, total, nb, nb + lane);
+            idx = nb + lane + __shfl(delta, owner);
+            if (nb + lane < total) ref = sc.refs[idx];
+        }
+        if (w < total) {
             float l = 0.f, bu, bv;
             bool h;
-            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
+            if (__builtin_expect((cur_ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
             else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
             if (h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
+                atomicMin(&g_coop_key[wbase + cur_owner], ((unsigned long long)__float_as_uint(l) << 32) | cur_idx);
         }
     }
     if (SLAB) __builtin_amdgcn_wave_barrier();  // every read of this round's slab before the next fill
@@ -870,8 +935,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         }
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
         if (!done) {
-            bool ret = false;
-            if (key != ~0ull) {  // the leaf's closest valid hit: re-test it for its barycentrics
+            // The leaf returns its closest valid hit iff l <= exit + EPS; the key holds l's bits
+            // (the re-test below computes the same l), so only a returning leaf re-tests its
+            // winner for the barycentrics (biplane's light sphere, in every leaf, used to be
+            // re-tested after every leaf).
+            bool ret = key != ~0ull && __uint_as_float((uint32_t)(key >> 32)) <= exit_t + EPS;
+            if (ret) {
                 const uint32_t ref = sc.refs[(uint32_t)key];
                 const float4* pd = prim_data(sc, ref);
                 const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
@@ -882,7 +951,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 best->l = l;
                 best->bu = bu;
                 best->bv = bv;
-                ret = l <= exit_t + EPS;
             }
             if (ret) {
                 done = true;
@@ -912,20 +980,169 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     return found;
 }
 
+// ------------------------------------------------------------ packet traversal (camera rays)
+// The scene arrays the packet traversal reads, as __restrict__ kernel arguments: loads from
+// them that are wave-uniform then compile to scalar loads (s_load), which take the scalar
+// memory path beside the vector-memory pipeline (TA/TD) that bounds the cooperative passes.
+struct PkScene {
+    const uint2* nodes;
+    const uint32_t* refs;
+    const float4* prim4;
+};
+
+// Camera rays of one wave traced as a packet: lanes `pk` share the signs of their (EPS-clamped)
+// directions, so every branch orders its children the same way for all of them.  The packet
+// walks the tree from the root, the wave-uniform node fetched by a scalar load, each lane
+// deciding near / far / both on its own interval exactly as kdtree.rs:79-87 does; where some
+// lanes need the near child, the lanes that need only the far one are deferred.  At the leaf the
+// lanes still active test its refs one at a time, the primitive in scalar registers (no
+// per-lane gather; the next ref's primitive is loaded during the current test), keeping the
+// first strict minimum (closest_hit.rs:25), and return it if l <= exit + EPS (kdtree.rs:96).
+// A lane that does not return restarts from the root with entry = that leaf's exit (kd-restart
+// with push-down, as in stack_search_coop); deferred lanes restart with their entry unchanged.
+// Either way a lane's next leaf and its interval are those of the reference's stack traversal,
+// bit for bit ("Packet traversal"), so each lane visits exactly its own leaves in
+// its own order.  Called by every lane of the wave.
+// A leaf visit costs the packet a descent and one test per ref at the whole wave's width, so
+// once fewer than RT_PACKET_KEEP lanes reach the packet's next leaf the packet stops: its lanes
+// still searching (`live`) continue in the cooperative search from interval [entry, root_exit],
+// where the reference's stack traversal visits the same remaining leaves (kd-restart argument).
+#ifndef RT_PACKET_KEEP
+#define RT_PACKET_KEEP 40
+#endif
+template <bool FAST>
+__device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax, bool pk, float& entry,
+                               float root_exit, Hit* best, bool& live) {
+    float exit_t = root_exit;
+    bool found = false;
+    live = pk;
+    const uint32_t lead = (uint32_t)__ffsll((unsigned long long)__ballot(pk)) - 1u;
+    // near child of a branch on axis a: low when the (shared) clamped d_a > 0
+    const uint32_t pos_bits = (uint32_t)__builtin_amdgcn_readlane(
+        (int)((ax.dx > 0.0f ? 1u : 0u) | (ax.dy > 0.0f ? 2u : 0u) | (ax.dz > 0.0f ? 4u : 0u)), (int)lead);
+    // Restart node: the deepest node a descent reached before any live lane pushed or was
+    // deferred.  Above it every live lane went near with its whole interval (t >= exit = root
+    // exit) or far with t <= entry, and still does with a larger entry, so all of their
+    // remaining intervals lie below it (the per-lane argument of stack_search_coop, for the
+    // packet as a whole); it only moves down.
+    uint32_t restart = 0;
+    while (__ballot(live)) {
+        bool act = live, pushed = false, clean = true;
+        uint32_t node = restart;
+        uint2 nd = ps.nodes[node];
+        while ((nd.y & 3u) != RT_KD_LEAF) {
+            float t = 0.f;
+            bool go_far = false, push = false;
+            if (act) {
+                float d;
+                t = split_t<FAST>(nd, ax, r, &d);
+                const bool go_near = t >= exit_t;
+                go_far = !go_near && t <= entry;
+                push = !go_near && !go_far;
+            }
+            const bool pos = (pos_bits >> (nd.y & 3u)) & 1u;
+            node = nd.y >> 2;
+            if (__ballot(act && !go_far)) {  // near child, with the lanes that need it
+                clean = clean && __ballot(act && (go_far || push)) == 0;
+                act = act && !go_far;
+                exit_t = act && push ? t : exit_t;
+                pushed = pushed || (act && push);
+                node += pos ? 0u : 1u;
+            } else {                          // every active lane goes far only
+                node += pos ? 1u : 0u;
+            }
+            restart = clean ? node : restart;
+            nd = ps.nodes[node];
+        }
+        if (RT_PACKET_KEEP > 0 && __popcll(__ballot(act)) < RT_PACKET_KEEP) break;
+        // the leaf: active lanes test every ref, first strict minimum
+        const uint32_t off = nd.y >> 2, cnt = nd.x & LEAF_COUNT_MASK;
+        bool lf = false;
+        float ll = 0.f, lu = 0.f, lv = 0.f;
+        uint32_t lref = 0;
+        uint32_t ref_n = ps.refs[off];  // uploads carry zero padding past the end
+        const float4* pn = ps.prim4 + 3 * (size_t)(ref_n & REF_INDEX_MASK);
+        float4 b0 = pn[0], b1 = pn[1], b2 = pn[2];
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t ref = ref_n;
+            const float4 a0 = b0, a1 = b1, a2 = b2;
+            if (j + 1 < cnt) {  // the next ref's primitive, in flight during this test
+                ref_n = ps.refs[off + j + 1];
+                pn = ps.prim4 + 3 * (size_t)(ref_n & REF_INDEX_MASK);
+                b0 = pn[0];
+                b1 = pn[1];
+                b2 = pn[2];
+            }
+            if (act) {
+                float l = 0.f, bu = 0.f, bv = 0.f;
+                bool h;
+                if ((ref >> REF_KIND_SHIFT) == K_SPHERE) h = sphere_hit(a0, r, &l);
+                else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
+                const bool take = h && l >= HIT_MIN && (!lf || l < ll);  // valid, not NaN, first minimum
+                ll = take ? l : ll;
+                lu = take ? bu : lu;
+                lv = take ? bv : lv;
+                lref = take ? ref : lref;
+                lf = lf || take;
+            }
+        }
+        if (act) {
+            if (lf && ll <= exit_t + EPS) {
+                best->ref = lref;
+                best->l = ll;
+                best->bu = lu;
+                best->bv = lv;
+                found = true;
+                live = false;
+            } else if (!pushed) {
+                live = false;  // the interval is exhausted: the reference's empty stack
+            } else {
+                entry = exit_t;
+            }
+        }
+        exit_t = root_exit;
+    }
+    return found;
+}
+
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
 template <bool RESTART, bool SLAB>
 __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
-                                             uint32_t* st, bool active) {
+                                             uint32_t* st, bool active, bool camera = false,
+                                             const PkScene* ps = nullptr) {
     float root_entry = 0.f, root_exit = 0.f;
     const RayAx ax = ray_axes(r);
     const bool in = active && sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit);
-    bool found;
+    bool found = false;
     const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
-    if (__builtin_expect(__ballot(!fast) == 0, 1))
-        found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in, root_entry, root_exit, best, st);
-    else
-        found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in, root_entry, root_exit, best, st);
+    const bool all_fast = __ballot(!fast) == 0;
+    bool pk = false, pk_live = false;
+    if (RT_PACKET && !SLAB && ps) {
+        // camera rays of the direction octant of the first one form the packet (NaN directions
+        // never: d > 0 and d < 0 are both false); the other lanes take the cooperative search
+        const uint32_t oct = (ax.dx > 0.0f ? 1u : 0u) | (ax.dy > 0.0f ? 2u : 0u) | (ax.dz > 0.0f ? 4u : 0u);
+        const bool num = !__builtin_isnan(ax.dx) && !__builtin_isnan(ax.dy) && !__builtin_isnan(ax.dz);
+        const bool cand = in && camera && num;
+        const uint64_t cm = __ballot(cand);
+        if (__popcll(cm) >= RT_PACKET_MIN) {
+            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)cm) - 1u;
+            pk = cand && oct == (uint32_t)__builtin_amdgcn_readlane((int)oct, (int)lead);
+            if (__popcll(__ballot(pk)) >= RT_PACKET_MIN) {
+                found = all_fast ? closest_packet<true>(*ps, r, ax, pk, root_entry, root_exit, best, pk_live)
+                                 : closest_packet<false>(*ps, r, ax, pk, root_entry, root_exit, best, pk_live);
+            } else {
+                pk = false;
+            }
+        }
+    }
+    const bool in_coop = in && (!pk || pk_live);
+    if (__ballot(in_coop)) {
+        if (__builtin_expect(all_fast, 1))
+            found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+        else
+            found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+    }
     if (found) return true;
     if (active && sc.has_cube) {
         best->ref = REF_CUBE;
@@ -1253,14 +1470,14 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
 
 template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool SLAB = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
-                                        Ctr<COUNT>& c, bool active = true) {
+                                        Ctr<COUNT>& c, bool active = true, const PkScene* ps = nullptr) {
     if (COUNT) c.segments++;
     // The ray's direction arrives un-normalized from camera_ray or shade: one normalize here
     // serves a wave's new paths and continued ones alike (each lane normalizes the same vector
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop<RESTART, SLAB>(sc, p.ray, &h, st, active)
+    const bool hit = COOP ? closest_coop<RESTART, SLAB>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
                           : closest<COUNT, GEN, RESTART>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
@@ -1421,7 +1638,9 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
 }
 
 template <bool GEN, bool DLS, bool RESTART, bool SLAB = false>
-__global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a) {
+__global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a, const uint2* __restrict__ pk_nodes,
+                                                                                const uint32_t* __restrict__ pk_refs,
+                                                                                const float4* __restrict__ pk_prim4) {
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
     if (!GEN) {  // only the sphere-only kernel reads the LDS sphere tables
@@ -1461,9 +1680,16 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                     uint32_t j, o;
                     split_item(a, item, &j, &o);
                     int x, y;
-                    launch_pixel(a, o, &x, &y);
+                    if (a.pix_q) {  // item j * n_pix + q: the q-th pixel in queue order
+                        const uint2 e = a.pix_q[o];
+                        x = (int)(e.x & 0xffffu);
+                        y = (int)(e.x >> 16);
+                        o = e.y;
+                    } else {
+                        launch_pixel(a, o, &x, &y);
+                    }
                     start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
-                    slot = item;
+                    slot = j * a.n_pix + o;
                     have = true;
                 } else {
                     done = true;
@@ -1481,7 +1707,8 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
-        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have) && have
+        const PkScene ps{pk_nodes, pk_refs, pk_prim4};
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
@@ -1588,7 +1815,8 @@ size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks) {
 
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
     return with_queue_kernel(a, [&](auto k, bool gen) {
-        hipLaunchKernelGGL(k, dim3(n_blocks), dim3(BLOCK), queue_lds_bytes(a, gen), s, a);
+        hipLaunchKernelGGL(k, dim3(n_blocks), dim3(BLOCK), queue_lds_bytes(a, gen), s, a, a.sc.nodes, a.sc.refs,
+                           a.sc.prim4);
         return hipGetLastError();
     });
 }
