@@ -35,6 +35,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+# rt_amd raises HIP's hardware queues per process (GPU_MAX_HW_QUEUES, before HIP starts) so that
+# the pipeline slots' streams overlap instead of sharing queues (launch pipeline)
+import rt_amd  # noqa: E402,F401
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s chip-wide

@@ -35,11 +35,14 @@ static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 // buffer, item counter and traversal-stack scratch: launch i + 1 starts while launch i drains
 // (its last paths finish on a few lanes), and only the folds, which update the shared
 // accumulators and the output, are chained in order by events.  A mesh launch's drain tail is
-// ~8-10 ms; a 1-spp a380 launch holds ~3 ms of work, so small launches need more of them in
-// flight to cover one tail: 3 slots for launches of up to 2^21 samples, else 2 (A/B over 2, 3
-// and 4 slots: a380 at 1 spp 143 / 189 / 164 Msamples/s; biplane at 10 spp 508 / 507 / 436;
-// spaceship at 25 spp 267 / 258 / 256).  RT_PIPELINE_SLOTS (2-4) fixes the count.
-constexpr int N_SLOTS = 4;
+// ~8-10 ms; a 1-spp a380 launch holds ~2 ms of work, so small launches need more of them in
+// flight to cover one tail: 8 slots for launches of up to 2^21 samples, else 2.  The slots'
+// streams overlap only on separate hardware queues: with HIP's default GPU_MAX_HW_QUEUES = 4,
+// a380 at 1 spp ran 187 Msamples/s whatever the slots; with 8 queues 2 / 4 / 6 slots ran
+// 137 / 229 / 272, with 12 queues and 8 slots 288 (rt_amd sets 12 before HIP starts).  Larger
+// launches: 2 slots (12 queues, biplane at 10 spp 590 / 587 / 569 with 2 / 3 / 4 slots).
+// RT_PIPELINE_SLOTS (2-8) fixes the count.
+constexpr int N_SLOTS = 8;
 constexpr uint64_t SMALL_LAUNCH_ITEMS = 1ull << 21;
 struct Slot {
     hipStream_t stream = nullptr;
@@ -391,19 +394,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
             pool[3 * t + 2] = make_float4(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z, 0.f);
         }
         if ((st = upload(c, pool, &d.prim4))) return st;
-        std::vector<float4> pool8(2 * (pool.size() / 3));
-        for (size_t t = 0; t < pool.size() / 3; ++t) {
-            const float4 v0 = pool[3 * t], e1 = pool[3 * t + 1], e2 = pool[3 * t + 2];
-            pool8[2 * t] = t < scene->n_spheres ? v0 : make_float4(v0.x, v0.y, v0.z, e1.x);
-            pool8[2 * t + 1] = t < scene->n_spheres ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(e1.y, e1.z, e2.x, e2.y);
-        }
-        std::vector<float> zref(refs.size());
-        for (size_t i = 0; i < refs.size(); ++i) {
-            const size_t t = refs[i] & REF_INDEX_MASK;
-            zref[i] = t < scene->n_spheres ? 0.f : pool[3 * t + 2].z;
-        }
-        if ((st = upload(c, pool8, &d.prim8))) return st;
-        if ((st = upload(c, zref, &d.zref))) return st;
         d.pool_ftri = scene->n_spheres;
         d.pool_mesh = scene->n_spheres + scene->n_free_tris;
     }
@@ -745,7 +735,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         // Overlapped launches alternate slots; a serialized one stays on the last slot's stream,
         // behind its fold, with one radiance buffer.
         const bool overlap = c->overlap && a.n_items <= c->overlap_max_items;
-        const uint32_t n_slots = c->n_slots ? c->n_slots : (a.n_items <= SMALL_LAUNCH_ITEMS ? 3u : 2u);
+        const uint32_t n_slots = c->n_slots ? c->n_slots : (a.n_items <= SMALL_LAUNCH_ITEMS ? (uint32_t)N_SLOTS : 2u);
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
         Slot& sl = c->slot[c->cur_slot];
         const uint64_t floats = 3 * n_out * (a.sample_count ? a.sample_count : 1);

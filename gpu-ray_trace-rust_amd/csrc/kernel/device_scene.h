@@ -88,10 +88,6 @@ struct DevScene {
     // subtraction generic.rs:104-105 performs per test.
     // A ref's index is its pool position; per-kind arrays below take index - pool_<kind>.
     const float4* prim4;
-    // RT_ZREF: the pool as two float4 per primitive, {v0, e1.x}, {e1.y, e1.z, e2.x, e2.y} (a
-    // sphere: {c, r}, 0), and e2.z in an array parallel to refs (zref[i] of refs[i])
-    const float4* prim8;
-    const float* zref;
     uint32_t pool_ftri, pool_mesh;
     // direct-light sampling (dir_light_samp): renderables in renderable order (device refs) and
     // the emissive spheres {sphere index, position in elem_refs}

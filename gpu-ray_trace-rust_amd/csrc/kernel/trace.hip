@@ -47,9 +47,6 @@
 #ifndef RT_OWNER_LOOP
 #define RT_OWNER_LOOP 8     // cooperative pass: owners of a pass found by a readlane loop when at most this many leaves end in it (0: binary search)
 #endif
-#ifndef RT_PIPE_REF
-#define RT_PIPE_REF 0       // cooperative pass: the next pass's owners and refs loaded before this pass's test
-#endif
 #ifndef RT_PACKET
 #define RT_PACKET 1         // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
 #endif
@@ -803,25 +800,17 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     }
     // item w of a lane's leaf is sc.refs[w + delta]
     const uint32_t delta = off - (incl - cnt);
-    constexpr bool PIPE = RT_PIPE_REF && !SLAB;
-    uint32_t owner = 0, idx = 0, ref = 0;
-    if (PIPE && total) {
-        owner = pass_owner(incl, total, 0u, lane);
-        idx = lane + __shfl(delta, owner);
-        if (lane < total) ref = sc.refs[idx];
-    }
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t w = base + lane;
-        if (!PIPE) {
-            owner = pass_owner(incl, total, base, w);
-            idx = w + __shfl(delta, owner);
-        }
+        const uint32_t owner = pass_owner(incl, total, base, w);
+        const uint32_t idx = w + __shfl(delta, owner);
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
         const uint32_t od = SLAB ? __shfl(sdelta, owner) : SLAB_NONE;
-        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
         if (w < total) {
+            uint32_t ref;
+            float4 a0, a1, a2;
             if (SLAB && od != SLAB_NONE) {
                 const float4* sp = g_slab[threadIdx.x >> 6] + 3 * (w + od);
                 a0 = sp[0];
@@ -831,42 +820,18 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             } else {
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
-                if (!PIPE) ref = sc.refs[idx];
-#if defined(RT_PROBE_NOREF)
-                ref = (K_MESH_TRI << REF_KIND_SHIFT) | (sc.pool_mesh + (idx & 1023u));
-#endif
-#if defined(RT_ZREF)
-                const float4* q = sc.prim8 + 2 * (size_t)(ref & REF_INDEX_MASK);
-                const float4 b0 = q[0], b1 = q[1];
-                a0 = b0;
-                a1 = make_float4(b0.w, b1.x, b1.y, 0.f);
-                a2 = make_float4(b1.z, b1.w, sc.zref[idx], 0.f);
-#else
+                ref = sc.refs[idx];
                 const float4* pd = prim_data(sc, ref);
                 a0 = pd[0];
                 a1 = pd[1];
-#if defined(RT_PROBE_NOA2)
-                a2 = a1;
-#else
                 a2 = pd[2];
-#endif
-#endif
             }
-        }
-        const uint32_t cur_owner = owner, cur_idx = idx, cur_ref = ref;
-        if (PIPE && base + 64u < total) {  // the next pass's owners and refs, in flight during this test
-            const uint32_t nb = base + 64u;
-            owner = pass_owner(incl, total, nb, nb + lane);
-            idx = nb + lane + __shfl(delta, owner);
-            if (nb + lane < total) ref = sc.refs[idx];
-        }
-        if (w < total) {
             float l = 0.f, bu, bv;
             bool h;
-            if (__builtin_expect((cur_ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
+            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
             else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
             if (h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&g_coop_key[wbase + cur_owner], ((unsigned long long)__float_as_uint(l) << 32) | cur_idx);
+                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
         }
     }
     if (SLAB) __builtin_amdgcn_wave_barrier();  // every read of this round's slab before the next fill

@@ -10,8 +10,8 @@ run() {  # name, bench args
 for mode in "" "--sync"; do
   tag=${mode:+_sync}
   run triangles$tag --scene triangles --steps 10 --warmup 2 $mode "$@"
-  run a380_b1$tag --scene a380 --steps 20 --warmup 3 $mode "$@"
-  run a380_b10$tag --scene a380 --spp-per-step 10 --steps 5 --warmup 1 $mode "$@"
+  run a380_b1$tag --scene a380 --steps 60 --warmup 3 $mode "$@"
+  run a380_b10$tag --scene a380 --spp-per-step 10 --steps 15 --warmup 2 $mode "$@"
   run biplane_b10$tag --scene biplane --steps 20 --warmup 3 $mode "$@"
   run spaceship_b25$tag --scene spaceship_r1 --steps 8 --warmup 2 $mode "$@"
   run spaceship4096_b25$tag --scene spaceship_r1 --width 4096 --height 4096 --steps 3 --warmup 1 $mode "$@"
