@@ -68,6 +68,21 @@ constexpr float RR_THRES = 0.4f;        // radiance.rs:77
 // It only guarantees that a corrupted scene cannot hang the GPU.
 constexpr int MAX_BOUNCES = 1024;
 
+// Diagnostic build only (-DRT_TIMING=1, tools/build_variants.sh): wave-clock split of the general
+// queue kernel, summed over waves and printed by the last wave of each launch.
+#ifndef RT_TIMING
+#define RT_TIMING 0
+#endif
+#if RT_TIMING
+__device__ unsigned long long g_tm[12];
+__device__ unsigned int g_tm_waves;
+#define TM_NOW() __builtin_amdgcn_s_memtime()
+#define TM_ADD(i, v) do { const unsigned long long tm_v_ = (unsigned long long)(v); if (__lane_id() == 0) atomicAdd(&g_tm[i], tm_v_); } while (0)
+#else
+#define TM_ADD(i, v) do { } while (0)
+#endif
+
+
 struct V3 {
     float x, y, z;
 };
@@ -667,6 +682,15 @@ __device__ __forceinline__ bool closest(const DevScene& sc, const Ray& r, Hit* b
     return false;
 }
 
+// The scene arrays the packet traversal reads, as __restrict__ kernel arguments: loads from
+// them that are wave-uniform then compile to scalar loads (s_load), which take the scalar
+// memory path beside the vector-memory pipeline (TA/TD) that bounds the cooperative passes.
+struct PkScene {
+    const uint2* nodes;
+    const uint32_t* refs;
+    const float4* prim4;
+};
+
 // ------------------------------------------------------------ cooperative leaf tests (meshes)
 // With one lane per ray, a wave tests leaf refs for as long as its *longest* leaf: mesh leaves
 // average ~23 refs and the longest of 64 is ~4x that, so 3/4 of the lanes idle (biplane: 24%
@@ -898,6 +922,16 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             off += lead;
             cnt -= lead;
         }
+        TM_ADD(9, 1);
+        TM_ADD(10, __popcll(__ballot(cnt > 0)));
+#if RT_TIMING
+        {   // leaf sharing: lanes at the leaf of the first lane with one
+            const uint64_t hv = __ballot(cnt > 0);
+            const uint32_t f = hv ? (uint32_t)__ffsll((unsigned long long)hv) - 1u : 0u;
+            const uint32_t fo = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)f);
+            TM_ADD(11, hv ? __popcll(__ballot(cnt > 0 && off == fo)) : 0);
+        }
+#endif
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
         if (!done) {
             // The leaf returns its closest valid hit iff l <= exit + EPS; the key holds l's bits
@@ -946,14 +980,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
 }
 
 // ------------------------------------------------------------ packet traversal (camera rays)
-// The scene arrays the packet traversal reads, as __restrict__ kernel arguments: loads from
-// them that are wave-uniform then compile to scalar loads (s_load), which take the scalar
-// memory path beside the vector-memory pipeline (TA/TD) that bounds the cooperative passes.
-struct PkScene {
-    const uint2* nodes;
-    const uint32_t* refs;
-    const float4* prim4;
-};
 
 // Camera rays of one wave traced as a packet: lanes `pk` share the signs of their (EPS-clamped)
 // directions, so every branch orders its children the same way for all of them.  The packet
@@ -975,6 +1001,10 @@ struct PkScene {
 #ifndef RT_PACKET_KEEP
 #define RT_PACKET_KEEP 40
 #endif
+#ifndef RT_PACKET_SIDE
+#define RT_PACKET_SIDE 1    // 1: at a branch the packet follows the child more of its active lanes need (the others deferred)
+#endif
+
 template <bool FAST>
 __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax, bool pk, float& entry,
                                float root_exit, Hit* best, bool& live) {
@@ -1007,32 +1037,42 @@ __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax,
             }
             const bool pos = (pos_bits >> (nd.y & 3u)) & 1u;
             node = nd.y >> 2;
-            if (__ballot(act && !go_far)) {  // near child, with the lanes that need it
+            const uint32_t n_near = (uint32_t)__popcll(__ballot(act && !go_far));
+            const uint32_t n_far = (uint32_t)__popcll(__ballot(act && go_far));
+            if (n_near && (!RT_PACKET_SIDE || n_near >= n_far)) {  // near child, with the lanes that need it
                 clean = clean && __ballot(act && (go_far || push)) == 0;
                 act = act && !go_far;
                 exit_t = act && push ? t : exit_t;
                 pushed = pushed || (act && push);
                 node += pos ? 0u : 1u;
-            } else {                          // every active lane goes far only
+            } else {  // far child, with the lanes that need only it; the others are deferred
+                clean = clean && n_near == 0;
+                act = act && go_far;
                 node += pos ? 1u : 0u;
             }
             restart = clean ? node : restart;
             nd = ps.nodes[node];
         }
         if (RT_PACKET_KEEP > 0 && __popcll(__ballot(act)) < RT_PACKET_KEEP) break;
+        TM_ADD(3, 1);
+        TM_ADD(4, __popcll(__ballot(act)));
+        TM_ADD(5, nd.x & LEAF_COUNT_MASK);
         // the leaf: active lanes test every ref, first strict minimum
         const uint32_t off = nd.y >> 2, cnt = nd.x & LEAF_COUNT_MASK;
         bool lf = false;
         float ll = 0.f, lu = 0.f, lv = 0.f;
         uint32_t lref = 0;
-        uint32_t ref_n = ps.refs[off];  // uploads carry zero padding past the end
+        // software pipeline: during the test of ref j, the primitive of ref j + 1 and the ref
+        // j + 2 are in flight (uploads carry zero padding past the end of refs)
+        uint32_t ref_n = ps.refs[off], ref_nn = ps.refs[off + 1];
         const float4* pn = ps.prim4 + 3 * (size_t)(ref_n & REF_INDEX_MASK);
         float4 b0 = pn[0], b1 = pn[1], b2 = pn[2];
         for (uint32_t j = 0; j < cnt; ++j) {
             const uint32_t ref = ref_n;
             const float4 a0 = b0, a1 = b1, a2 = b2;
-            if (j + 1 < cnt) {  // the next ref's primitive, in flight during this test
-                ref_n = ps.refs[off + j + 1];
+            if (j + 1 < cnt) {
+                ref_n = ref_nn;
+                ref_nn = ps.refs[off + j + 2];
                 pn = ps.prim4 + 3 * (size_t)(ref_n & REF_INDEX_MASK);
                 b0 = pn[0];
                 b1 = pn[1];
@@ -1083,6 +1123,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
     const bool all_fast = __ballot(!fast) == 0;
     bool pk = false, pk_live = false;
+#if RT_TIMING
+    const unsigned long long tm0 = TM_NOW();
+#endif
     if (RT_PACKET && !SLAB && ps) {
         // camera rays of the direction octant of the first one form the packet (NaN directions
         // never: d > 0 and d < 0 are both false); the other lanes take the cooperative search
@@ -1102,12 +1145,22 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
         }
     }
     const bool in_coop = in && (!pk || pk_live);
+#if RT_TIMING
+    const unsigned long long tm1 = TM_NOW();
+    TM_ADD(0, tm1 - tm0);
+    TM_ADD(6, __popcll(__ballot(pk)));
+    TM_ADD(7, __popcll(__ballot(pk && pk_live)));
+    TM_ADD(8, __popcll(__ballot(in_coop)));
+#endif
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
             found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
         else
             found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
     }
+#if RT_TIMING
+    TM_ADD(1, TM_NOW() - tm1);
+#endif
     if (found) return true;
     if (active && sc.has_cube) {
         best->ref = REF_CUBE;
@@ -1608,6 +1661,9 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                                                                                 const float4* __restrict__ pk_prim4) {
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
+#if RT_TIMING
+    const unsigned long long tm_start = TM_NOW();
+#endif
     if (!GEN) {  // only the sphere-only kernel reads the LDS sphere tables
         fill_lds_spheres(sc);
         __syncthreads();
@@ -1669,6 +1725,18 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             }
         }
         if (__ballot(have) == 0) {
+#if RT_TIMING
+            TM_ADD(2, TM_NOW() - tm_start);
+            if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+                __threadfence();
+                printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
+                       "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu\n",
+                       g_tm[0], g_tm[1], g_tm[2], g_tm[3], g_tm[4], g_tm[5], g_tm[6], g_tm[7], g_tm[8], g_tm[9],
+                       g_tm[10], g_tm[11]);
+                for (int i = 0; i < 12; ++i) g_tm[i] = 0;
+                g_tm_waves = 0;
+            }
+#endif
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
