@@ -120,6 +120,14 @@ def roofline(scene, per_launch, kernel_ms, build_id, kernel):
              "note": "rocprofv3 FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md), own pass"}
         out["hbm"] = h
         fr["hbm"] = h
+    if d.get("td_busy_frac"):
+        # the vector-memory pipeline: fraction of the kernel's cycles the per-CU texture-data unit
+        # (the return path of every global / scratch load) is busy; the mesh kernels' limiter
+        v = {"achieved": d["td_busy_frac"], "peak": 1.0, "unit": "fraction of cycles TD busy",
+             "frac": d["td_busy_frac"], "ta_busy_frac": d.get("ta_busy_frac"),
+             "note": "rocprofv3 TD_TD_BUSY_sum / 256 CUs over GRBM_GUI_ACTIVE / 8 XCDs, own pass"}
+        out["vmem"] = v
+        fr["vmem"] = v
     if d.get("l2_bytes_per_launch"):
         b = d["l2_bytes_per_launch"]
         out["l2"] = {"achieved": round(b / sec / 1e9, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",

@@ -77,6 +77,7 @@ struct rt_ctx {
     uint32_t d_tiles_cap = 0;
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
     uint2* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
+    uint32_t pix_block = 1;           // RT_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
     float4* d_out = nullptr;
@@ -493,6 +494,16 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     // per sample, runs stackless and needs no global stack.  RT_KD_RESTART=0/1 overrides.
     // RT_KD_RESTART=2: stackless with the wave's leaf triangles staged in LDS per round (the
     // general kernel; measured slower).
+    // Camera-ray packets in the general queue kernel (trace.hip closest_packet), bit-identical to
+    // the cooperative search; RT_PACKET=0 turns them off.  RT_PIX_BLOCK=1 gives the queue the
+    // launch pixels in row order instead of 8 x 8 blocks (the same images).
+    d.packet = 1u;
+    if (const char* e = std::getenv("RT_PACKET")) d.packet = std::strcmp(e, "0") ? 1u : 0u;
+    c->pix_block = RT_PIX_BLOCK;
+    if (const char* e = std::getenv("RT_PIX_BLOCK")) {
+        const unsigned long v = std::strtoul(e, nullptr, 10);
+        if (v >= 1 && v <= 64) c->pix_block = (uint32_t)v;
+    }
     d.restart = d.spheres_only ? 1u : 0u;
     if (const char* e = std::getenv("RT_KD_RESTART")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
@@ -621,7 +632,7 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
             // queue order: RT_PIX_BLOCK x RT_PIX_BLOCK blocks of each tile, row by row
             std::vector<uint2> pq;
             pq.reserve(pix);
-            constexpr uint32_t B = RT_PIX_BLOCK > 0 ? RT_PIX_BLOCK : 1;
+            const uint32_t B = c->pix_block;
             for (const DevTile& d : dt)
                 for (uint32_t by = 0; by < d.h; by += B)
                     for (uint32_t bx = 0; bx < d.w; bx += B)
@@ -647,7 +658,7 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
         c->pixmap_tiles = dt;
     }
     a->pix_xy = (c->sc.width <= 65535u && c->sc.height <= 65535u) ? c->d_pixmap : nullptr;
-    a->pix_q = (a->pix_xy && RT_PIX_BLOCK > 1) ? c->d_pixq : nullptr;
+    a->pix_q = (a->pix_xy && c->pix_block > 1) ? c->d_pixq : nullptr;
     a->sc = c->sc;
     a->tiles = c->d_tiles;
     a->n_tiles = n_tiles;

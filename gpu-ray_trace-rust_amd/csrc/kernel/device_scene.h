@@ -76,6 +76,7 @@ struct DevScene {
     uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
     uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
     uint32_t restart;       // queue kernels: 0 stack, 1 stackless (kd-restart with push-down), 2 stackless + LDS triangle slabs
+    uint32_t packet;        // general queue kernel: camera rays may be traced as packets (closest_packet)
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

@@ -1126,7 +1126,7 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
 #if RT_TIMING
     const unsigned long long tm0 = TM_NOW();
 #endif
-    if (RT_PACKET && !SLAB && ps) {
+    if (RT_PACKET && !SLAB && ps && sc.packet) {
         // camera rays of the direction octant of the first one form the packet (NaN directions
         // never: d > 0 and d < 0 are both false); the other lanes take the cooperative search
         const uint32_t oct = (ax.dx > 0.0f ? 1u : 0u) | (ax.dy > 0.0f ? 2u : 0u) | (ax.dz > 0.0f ? 4u : 0u);

@@ -446,3 +446,26 @@ def test_stackless_traversal_bit_invariant(gpu_available, monkeypatch, scene_nam
             imgs[rs] = c.render(tiles, 0, spp)
     assert np.array_equal(imgs["0"], imgs["1"]), parity.stats(imgs["1"], imgs["0"])
     assert np.array_equal(imgs["0"], imgs["2"]), parity.stats(imgs["2"], imgs["0"])
+
+
+@pytest.mark.parametrize("scene_name,spp", [("triangles", 4), ("biplane", 3), ("spaceship_r1", 3), ("a380", 2)])
+def test_packet_traversal_bit_invariant(gpu_available, monkeypatch, scene_name, spp):
+    """Camera-ray packets (closest_packet: scalar-loaded nodes and leaf refs, per-lane
+    near / far / push on the lane's own interval, deferred lanes, kd-restart from the packet's
+    restart node, hand-over to the cooperative search) and the 8 x 8 block queue order give the
+    cooperative search's images bit for bit (kdtree.rs:66-104), on two tiles and a full frame."""
+    from rt_amd import render
+
+    sc = load_scene(scene_name, width=320, height=160)
+    w, h = sc.info.width, sc.info.height
+    tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
+    imgs = {}
+    for cfg in (("1", "8"), ("0", "1"), ("1", "1"), ("0", "8")):
+        monkeypatch.setenv("RT_PACKET", cfg[0])
+        monkeypatch.setenv("RT_PIX_BLOCK", cfg[1])
+        with render.Context(sc) as c:
+            imgs[cfg] = (c.render(tiles, 0, spp), c.render(None, spp, spp))
+    ref = imgs[("1", "8")]
+    for cfg, got in imgs.items():
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b), (cfg, parity.stats(a, b))

@@ -52,7 +52,8 @@ def main(tag):
                 lines += ["## bench.py line (under the profiler)", "", "```", l.strip(), "```", ""]
     cnt = {}
     for part, title in (("fetch", "HBM read bytes (FETCH_SIZE, own pass)"), ("sq", "SQ counters (own pass)"),
-                        ("sq2", "SQ lane utilisation (own pass)"), ("tcc", "L2 hits / misses (TCC, own pass)")):
+                        ("sq2", "SQ lane utilisation (own pass)"), ("tcc", "L2 hits / misses (TCC, own pass)"),
+                        ("tatd", "Vector-memory units busy (TA / TD, own pass)")):
         p = os.path.join(src, part, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -92,6 +93,15 @@ def main(tag):
             cnt["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(req, 1), 4)
             lines.append(f"\nLast dispatch: L2 hit rate {cnt['l2_hit_rate']:.1%}, {req:.4g} requests "
                          f"(x 128 B = {128 * req / 1e9:.3f} GB).")
+        if "TD_TD_BUSY_sum" in d and d.get("GRBM_GUI_ACTIVE"):
+            # per-instance busy cycles (one TA / TD per CU) over the kernel's cycles per XCD
+            # (rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs, MI355X_MICROARCH.md)
+            cyc = d["GRBM_GUI_ACTIVE"] / 8
+            cnt["td_busy_frac"] = round(d["TD_TD_BUSY_sum"] / 256 / cyc, 4)
+            cnt["ta_busy_frac"] = round(d.get("TA_TA_BUSY_sum", 0) / 256 / cyc, 4)
+            lines.append(f"\nLast dispatch: texture data (TD) busy {cnt['td_busy_frac']:.1%}, texture address (TA) "
+                         f"busy {cnt['ta_busy_frac']:.1%} of the kernel's cycles (per-CU unit, 256 CUs; "
+                         f"GRBM_GUI_ACTIVE / 8 XCDs).")
         lines.append("")
     if cnt:
         bid = os.path.join(src, "build_id")

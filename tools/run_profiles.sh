@@ -4,6 +4,7 @@
 #   2) FETCH_SIZE (HBM read bytes; x2 on gfx950 per MI355X_MICROARCH.md §HBM) in its own pass,
 #   3) SQ occupancy / stall / VALU counters and lane utilisation in their own passes,
 #   4) L2 (TCC) hits and misses in its own pass,
+#   5) the vector-memory units' busy cycles (TA address, TD data return) in its own pass,
 # plus the device-code build id the counters belong to (rt_amd.abi.kernel_build_id).
 # Counter passes run the bench synchronously (--sync): one trace dispatch at a time.
 # Usage: tools/run_profiles.sh <tag> [bench args...]; then python tools/prof_summary.py <tag>
@@ -24,4 +25,6 @@ timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_I
     python3 bench.py $ARGS --sync --no-cpu --no-roofline > $OUT/bench_sq2.log 2>&1 || exit 5
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/tcc -o run -- \
     python3 bench.py $ARGS --sync --no-cpu --no-roofline > $OUT/bench_tcc.log 2>&1 || exit 6
+timeout -k 10 300 rocprofv3 --pmc TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/tatd -o run -- \
+    python3 bench.py $ARGS --sync --no-cpu --no-roofline > $OUT/bench_tatd.log 2>&1 || exit 7
 echo profiles_ok $TAG
