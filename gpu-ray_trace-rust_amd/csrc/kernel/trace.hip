@@ -74,7 +74,7 @@ constexpr int MAX_BOUNCES = 1024;
 #define RT_TIMING 0
 #endif
 #if RT_TIMING
-__device__ unsigned long long g_tm[12];
+__device__ unsigned long long g_tm[16];
 __device__ unsigned int g_tm_waves;
 #define TM_NOW() __builtin_amdgcn_s_memtime()
 #define TM_ADD(i, v) do { const unsigned long long tm_v_ = (unsigned long long)(v); if (__lane_id() == 0) atomicAdd(&g_tm[i], tm_v_); } while (0)
@@ -932,7 +932,14 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             TM_ADD(11, hv ? __popcll(__ballot(cnt > 0 && off == fo)) : 0);
         }
 #endif
+#if RT_TIMING
+        const unsigned long long tmc0 = TM_NOW();
+#endif
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
+#if RT_TIMING
+        TM_ADD(12, TM_NOW() - tmc0);
+        TM_ADD(13, (__shfl(wave_incl_scan(cnt, lane), 63) + 63u) / 64u);
+#endif
         if (!done) {
             // The leaf returns its closest valid hit iff l <= exit + EPS; the key holds l's bits
             // (the re-test below computes the same l), so only a returning leaf re-tests its
@@ -1730,10 +1737,10 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
                 __threadfence();
                 printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
-                       "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu\n",
+                       "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu | passes_time %llu passes %llu\n",
                        g_tm[0], g_tm[1], g_tm[2], g_tm[3], g_tm[4], g_tm[5], g_tm[6], g_tm[7], g_tm[8], g_tm[9],
-                       g_tm[10], g_tm[11]);
-                for (int i = 0; i < 12; ++i) g_tm[i] = 0;
+                       g_tm[10], g_tm[11], g_tm[12], g_tm[13]);
+                for (int i = 0; i < 16; ++i) g_tm[i] = 0;
                 g_tm_waves = 0;
             }
 #endif
