@@ -12,8 +12,12 @@
 // (sphere.rs, triangle/generic.rs, mesh/triangle.rs, distant_cube_map.rs, material/*.rs).
 //
 // Two instantiations: GEN = false for sphere-only scenes (walled.yml: spheres and materials in
-// LDS, the exact brute-force bound closest_small), GEN = true for triangles and meshes (the
-// wave tests its lanes' KD leaves cooperatively, stack_search_coop).  trace_kernel (one lane
+// LDS, the exact brute-force bound closest_small), GEN = true for triangles and meshes: a wave's
+// camera rays of one direction octant walk the tree as a packet, with wave-uniform nodes and
+// triangles in scalar registers (closest_packet), and every other search tests the lanes' KD
+// leaves cooperatively, all (ray, ref) pairs of the wave spread over its 64 lanes
+// (stack_search_coop).  Both are bit-identical to the reference's per-ray stack traversal.
+// The queue hands out a launch's pixels in 8 x 8 blocks (LaunchArgs::pix_q).  trace_kernel (one lane
 // per pixel, running mean in registers) is the direct schedule kept as the tests' second path
 // and, with COUNT, the work counter behind the roofline's algorithmic bytes.
 //
