@@ -83,7 +83,14 @@ constexpr int MAX_BOUNCES = 1024;
 #if RT_TIMING
 __device__ unsigned long long g_tm[16];
 __device__ unsigned int g_tm_waves;
-#define TM_NOW() __builtin_amdgcn_s_memtime()
+__device__ __forceinline__ unsigned long long tm_now() {  // ordered stamp (cdna guide §7)
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define TM_NOW() tm_now()
 #define TM_ADD(i, v) do { const unsigned long long tm_v_ = (unsigned long long)(v); if (__lane_id() == 0) atomicAdd(&g_tm[i], tm_v_); } while (0)
 #else
 #define TM_ADD(i, v) do { } while (0)
