@@ -102,3 +102,20 @@ def test_create_without_device_fails_cleanly(rtlib, walled):
     ctx = C.c_void_p()
     st = rtlib.rt_create(C.byref(walled.desc), C.byref(walled.cam), C.byref(walled.info), None, 0, C.byref(ctx))
     assert st == abi.RT_ERR_NO_DEVICE and not ctx.value
+
+
+@pytest.mark.parametrize("before,after", [(None, "12"), ("4", "12"), ("16", "16"), ("junk", "12")])
+def test_hw_queues_raised_before_hip_starts(before, after):
+    """Importing rt_amd raises GPU_MAX_HW_QUEUES to at least 12 (the launch pipeline's streams
+    each need a hardware queue) and keeps a higher value."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    if before is not None:
+        env["GPU_MAX_HW_QUEUES"] = before
+    code = ("import os, sys; sys.path.insert(0, %r); import rt_amd; print(os.environ['GPU_MAX_HW_QUEUES'])"
+            % os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == after
