@@ -5,6 +5,7 @@
 // -ffp-contract=off, like the oracle.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -971,33 +972,45 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
     const rt_tile full{0, 0, info->width, info->height};
     const uint64_t npix = (uint64_t)info->width * info->height;
     std::vector<float> rgba(npix * 4);
-    float4* dbuf[2] = {nullptr, nullptr};
-    hipEvent_t done[2] = {nullptr, nullptr};
+    // Batches in flight: batch i + AHEAD is enqueued before batch i is read back, each into its
+    // own output buffer, so the launch pipeline's slots stay busy (a 1-spp batch holds ~2 ms of
+    // work against a ~10 ms drain tail); the hook still sees every batch, in order.
+    constexpr uint32_t AHEAD = (uint32_t)N_SLOTS - 1u;
+    const uint32_t n_batch = spp / batch;
+    const uint32_t ring = std::min(AHEAD, n_batch ? n_batch - 1u : 0u) + 1u;
+    std::vector<float4*> dbuf(ring, nullptr);
+    std::vector<hipEvent_t> done(ring, nullptr);
     auto run = [&]() -> int {
-        for (int k = 0; k < 2; ++k) {
+        for (uint32_t k = 0; k < ring; ++k) {
             if (hipMalloc(&dbuf[k], npix * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "output alloc failed");
             HIPCHK(c, hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
         }
-        auto deliver = [&](uint32_t s_end, int k) -> int {
+        auto deliver = [&](uint32_t b) -> int {  // batch b's frame: samples [0, (b + 1) * batch)
+            const uint32_t k = b % ring;
             HIPCHK(c, hipEventSynchronize(done[k]));
             HIPCHK(c, hipMemcpy(rgba.data(), dbuf[k], npix * sizeof(float4), hipMemcpyDeviceToHost));
             rt_rgba_to_u8(rgba.data(), npix, target);
-            if (hook) hook(user, s_end);
+            if (hook) hook(user, (b + 1) * batch);
             return RT_OK;
         };
-        uint32_t i = 0;
-        for (uint32_t s = 0; s < spp; s += batch, ++i) {
-            int r = render_impl(c, &full, 1, s, batch, dbuf[i % 2], nullptr);
+        for (uint32_t i = 0; i < n_batch; ++i) {
+            if (i >= ring) {  // its buffer's previous batch first
+                int r = deliver(i - ring);
+                if (r) return r;
+            }
+            int r = render_impl(c, &full, 1, i * batch, batch, dbuf[i % ring], nullptr);
             if (r) return r;
-            HIPCHK(c, hipEventRecord(done[i % 2], c->slot[c->cur_slot].stream));
-            if (i > 0 && (r = deliver(s, (i - 1) % 2))) return r;
+            HIPCHK(c, hipEventRecord(done[i % ring], c->slot[c->cur_slot].stream));
         }
-        if (i > 0) return deliver(spp, (i - 1) % 2);
+        for (uint32_t b = n_batch > ring ? n_batch - ring : 0u; b < n_batch; ++b) {
+            int r = deliver(b);
+            if (r) return r;
+        }
         return RT_OK;
     };
     st = run();
     if (!st) st = sync_all(c);
-    for (int k = 0; k < 2; ++k) {
+    for (uint32_t k = 0; k < ring; ++k) {
         if (done[k]) (void)hipEventDestroy(done[k]);
         if (dbuf[k]) {
             (void)sync_all(c);

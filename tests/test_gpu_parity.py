@@ -413,18 +413,20 @@ def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, sp
     assert np.array_equal(got, ref)
 
 
-def test_render_to_target_pipelined_equals_batches(gpu_available):
-    """rt_render_to_target enqueues batch i + 1 before reading back batch i: every RGBA8 frame
-    handed to the update hook equals the synchronous batch loop's."""
+@pytest.mark.parametrize("scene_name,spp,batch", [("walled", 6, 2), ("biplane", 12, 1)])
+def test_render_to_target_pipelined_equals_batches(gpu_available, scene_name, spp, batch):
+    """rt_render_to_target keeps up to 7 batches in flight (each into its own output buffer,
+    reused after its read-back): every RGBA8 frame handed to the update hook, in order, equals
+    the synchronous batch loop's."""
     from rt_amd import render
 
-    sc = load_scene("walled", width=160, height=96)
+    sc = load_scene(scene_name, width=160, height=96)
     frames = []
-    render.render_to_target(sc, 6, 2, update_hook=lambda t, done: frames.append((done, t.copy())))
-    assert [d for d, _ in frames] == [2, 4, 6]
+    render.render_to_target(sc, spp, batch, update_hook=lambda t, done: frames.append((done, t.copy())))
+    assert [d for d, _ in frames] == list(range(batch, spp + 1, batch))
     with render.Context(sc) as c:
-        for i, s0 in enumerate(range(0, 6, 2)):
-            img = c.render(None, s0, 2)
+        for i, s0 in enumerate(range(0, spp, batch)):
+            img = c.render(None, s0, batch)
             assert np.array_equal(frames[i][1].reshape(-1, 4), render.rgba_to_u8(img)), s0
 
 
