@@ -1712,7 +1712,14 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
+#if RT_TIMING
+    // sphere-only kernel: wave clock in path starts, normalize, closest hit and shading
+    unsigned long long tq_regen = 0, tq_norm = 0, tq_closest = 0, tq_shade = 0, tq_seg = 0;
+#endif
     for (;;) {
+#if RT_TIMING
+        const unsigned long long tq0 = TM_NOW();
+#endif
         const uint64_t need = __ballot(!have && !done);
         // Starting paths is wave-wide work at the width of the idle lanes: in the sphere-only
         // kernel ~10 of 64 lanes end a path per segment, so it waits for RT_REGEN_MIN of them.
@@ -1758,9 +1765,19 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                 pool += n;
             }
         }
+#if RT_TIMING
+        tq_regen += TM_NOW() - tq0;
+#endif
         if (__ballot(have) == 0) {
 #if RT_TIMING
             TM_ADD(2, TM_NOW() - tm_start);
+            if (!GEN) {
+                TM_ADD(0, tq_regen);
+                TM_ADD(1, tq_norm);
+                TM_ADD(3, tq_closest);
+                TM_ADD(4, tq_shade);
+                TM_ADD(5, tq_seg);
+            }
             if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
                 __threadfence();
                 printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
@@ -1775,8 +1792,29 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
+#if RT_TIMING
+        bool fin = false;
+        if (GEN) {
+            fin = segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have;
+        } else {
+            tq_seg += 1;
+            const unsigned long long t0 = TM_NOW();
+            if (have) p.ray.d = normalize(p.ray.d);
+            const unsigned long long t1 = TM_NOW();
+            Hit h;
+            bool hit = false;
+            if (have) hit = closest<false, GEN, RESTART>(sc, p.ray, &h, st, c);
+            const unsigned long long t2 = TM_NOW();
+            if (have) fin = shade<false, GEN, DLS>(sc, p, h, hit, c);
+            const unsigned long long t3 = TM_NOW();
+            tq_norm += t1 - t0;
+            tq_closest += t2 - t1;
+            tq_shade += t3 - t2;
+        }
+#else
         const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
+#endif
         if (fin) {
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;

@@ -1,4 +1,6 @@
-# Wave-clock split of the general queue kernel (diagnostic build -DRT_TIMING=1 as lib/variants/librt_tm.so)
+# Wave-clock split of the queue kernels (diagnostic build -DRT_TIMING=1 as lib/variants/librt_tm.so);
+# walled: python tools/variant_bench.py --scene walled --spp 200 --rounds 1 tm (path starts,
+# normalize, closest hit, shading, segments in the packet..pk_refs columns)
 set -o pipefail
 mkdir -p gpurun_out
 for s in biplane spaceship_r1 a380; do
