@@ -57,6 +57,9 @@
 #ifndef RT_PACKET
 #define RT_PACKET 1         // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
 #endif
+#ifndef RT_LEAF_REUSE
+#define RT_LEAF_REUSE 1     // cooperative search: a leaf whose ref list is the previous leaf's reuses its minimum
+#endif
 #ifndef RT_PACKET_MIN
 #define RT_PACKET_MIN 40    // fewest camera rays of one direction octant that form a packet
 #endif
@@ -897,8 +900,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     int sp = 0;
     bool done = !active, found = false, pushed = false;
     const uint32_t lane = __lane_id();
+    // RT_LEAF_REUSE: the previous leaf's list (its offset in sc.refs: the upload gives identical
+    // lists one copy, so equal offsets mean equal lists) and its minimum key
+    uint32_t prev_list = ~0u;
+    unsigned long long prev_key = ~0ull;
     while (__ballot(!done) != 0) {
-        uint32_t off = 0, cnt = 0;
+        uint32_t off = 0, cnt = 0, list = ~0u;
         unsigned long long key0 = ~0ull;
         if (!done) {
             uint2 nd = fetch_node(sc, node);
@@ -940,14 +947,23 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             // tests; the wave's passes then hold triangles only, with no sphere / triangle split.
             off = nd.y >> 2;
             cnt = nd.x & LEAF_COUNT_MASK;
-            const uint32_t lead = nd.x >> LEAF_LEAD_SHIFT;
-            for (uint32_t j = 0; j < lead; ++j) {
-                float l;
-                if (sphere_hit(prim_data(sc, sc.refs[off + j])[0], r, &l) && l >= HIT_MIN)
-                    key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
+            list = off;
+            if (RT_LEAF_REUSE && cnt && off == prev_list) {
+                // The same ray against the same refs in the same order: every length, and so
+                // the first strict minimum and its position, is the previous leaf's.  Only the
+                // return test below (this leaf's exit) differs.
+                key0 = prev_key;
+                cnt = 0;
+            } else {
+                const uint32_t lead = nd.x >> LEAF_LEAD_SHIFT;
+                for (uint32_t j = 0; j < lead; ++j) {
+                    float l;
+                    if (sphere_hit(prim_data(sc, sc.refs[off + j])[0], r, &l) && l >= HIT_MIN)
+                        key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
+                }
+                off += lead;
+                cnt -= lead;
             }
-            off += lead;
-            cnt -= lead;
         }
         TM_ADD(9, 1);
         TM_ADD(10, __popcll(__ballot(cnt > 0)));
@@ -968,6 +984,10 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         TM_ADD(13, (__shfl(wave_incl_scan(cnt, lane), 63) + 63u) / 64u);
 #endif
         if (!done) {
+            if (RT_LEAF_REUSE) {
+                prev_list = list;
+                prev_key = key;
+            }
             // The leaf returns its closest valid hit iff l <= exit + EPS; the key holds l's bits
             // (the re-test below computes the same l), so only a returning leaf re-tests its
             // winner for the barycentrics (biplane's light sphere, in every leaf, used to be
