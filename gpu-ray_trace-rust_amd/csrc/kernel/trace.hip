@@ -904,6 +904,30 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     // lists one copy, so equal offsets mean equal lists) and its minimum key
     uint32_t prev_list = ~0u;
     unsigned long long prev_key = ~0ull;
+    // After a leaf that does not return: the reference's pop (or the kd-restart); false when the
+    // interval is exhausted (the reference's empty stack).
+    auto advance = [&]() -> bool {
+        if (RESTART ? !pushed : sp == 0) return false;
+        if (RESTART) {
+            entry = exit_t;
+            exit_t = root_exit;
+            node = restart;
+        } else {
+            --sp;
+            const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
+            float d;
+            (void)split_t<FAST>(pn, ax, r, &d);
+            node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
+            entry = top_t;
+            if (sp) {
+                top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
+                exit_t = top_t;
+            } else {
+                exit_t = root_exit;
+            }
+        }
+        return true;
+    };
     while (__ballot(!done) != 0) {
         uint32_t off = 0, cnt = 0, list = ~0u;
         unsigned long long key0 = ~0ull;
@@ -943,18 +967,18 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                     nd = fetch_node(sc, node);
                 }
             }
-            // The leaf's leading spheres (a scene's lights span most leaves) are this lane's own
-            // tests; the wave's passes then hold triangles only, with no sphere / triangle split.
             off = nd.y >> 2;
             cnt = nd.x & LEAF_COUNT_MASK;
             list = off;
             if (RT_LEAF_REUSE && cnt && off == prev_list) {
                 // The same ray against the same refs in the same order: every length, and so
-                // the first strict minimum and its position, is the previous leaf's.  Only the
-                // return test below (this leaf's exit) differs.
+                // the first strict minimum and its position, is the previous leaf's.  Only
+                // the return test (this leaf's exit) differs.
                 key0 = prev_key;
                 cnt = 0;
             } else {
+                // The leaf's leading spheres (a scene's lights span most leaves) are this
+                // lane's own tests; the wave's passes then hold triangles only.
                 const uint32_t lead = nd.x >> LEAF_LEAD_SHIFT;
                 for (uint32_t j = 0; j < lead; ++j) {
                     float l;
@@ -1004,29 +1028,10 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 best->l = l;
                 best->bu = bu;
                 best->bv = bv;
-            }
-            if (ret) {
                 done = true;
                 found = true;
-            } else if (RESTART ? !pushed : sp == 0) {
+            } else if (!advance()) {
                 done = true;
-            } else if (RESTART) {
-                entry = exit_t;
-                exit_t = root_exit;
-                node = restart;
-            } else {
-                --sp;
-                const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
-                float d;
-                (void)split_t<FAST>(pn, ax, r, &d);
-                node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
-                entry = top_t;
-                if (sp) {
-                    top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
-                    exit_t = top_t;
-                } else {
-                    exit_t = root_exit;
-                }
             }
         }
     }
