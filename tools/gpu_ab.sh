@@ -5,7 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 run() {  # scene spp
-  timeout -k 10 300 python -u tools/variant_bench.py --scene $1 --spp $2 --rounds 3 "${@:3}" 2>&1 | grep -v Warning | tee -a gpurun_out/ab.log || exit 1
+  timeout -k 10 300 python -u tools/variant_bench.py --scene $1 --spp $2 --rounds 3 "${@:3}" 2>&1 | grep --line-buffered -v Warning | tee -a gpurun_out/ab.log || exit 1
 }
 run walled 1000 "$@"
 run biplane 40 "$@"
