@@ -1706,6 +1706,12 @@ __device__ __forceinline__ void launch_pixel(const LaunchArgs& a, uint32_t o, in
 #ifndef RT_QMIN_SPH
 #define RT_QMIN_SPH 256
 #endif
+// A grab must cover every lane of a wave that asks at once (up to 64 items: queue_kernel claims
+// at most one grab per refill), and grabs stay multiples of 64.
+static_assert(RT_QMIN >= 64 && RT_QMIN % 64 == 0, "RT_QMIN: a multiple of 64, at least 64");
+static_assert(RT_QMIN_SPH >= 64 && RT_QMIN_SPH % 64 == 0, "RT_QMIN_SPH: a multiple of 64, at least 64");
+static_assert(RT_QMAX >= RT_QMIN && RT_QMAX >= RT_QMIN_SPH && RT_QMAX % 64 == 0 && RT_QMAX <= 1024,
+              "RT_QMAX: a multiple of 64 in [RT_QMIN, 1024] (the queue counter's overshoot bound)");
 template <bool GEN>
 __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_waves) {
     constexpr uint32_t qmin = GEN ? (uint32_t)RT_QMIN : (uint32_t)RT_QMIN_SPH;
