@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../../include/rt_abi.h"
+#include "../../../include/rt_rng.h"
 #include "../kernel/device_scene.h"
 #ifndef RT_LDS_SPHERES
 #define RT_LDS_SPHERES 64  // must match trace.hip
@@ -77,7 +78,7 @@ struct rt_ctx {
     DevTile* d_tiles = nullptr;
     uint32_t d_tiles_cap = 0;
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
-    uint2* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
+    uint4* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
     uint32_t pix_block = 1;           // RT_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
@@ -631,7 +632,7 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                 for (uint32_t y = 0; y < d.h; ++y)
                     for (uint32_t x = 0; x < d.w; ++x) pm[d.out_off + (size_t)y * d.w + x] = ((d.y0 + y) << 16) | (d.x0 + x);
             // queue order: RT_PIX_BLOCK x RT_PIX_BLOCK blocks of each tile, row by row
-            std::vector<uint2> pq;
+            std::vector<uint4> pq;
             pq.reserve(pix);
             const uint32_t B = c->pix_block;
             for (const DevTile& d : dt)
@@ -640,7 +641,9 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                         for (uint32_t y = by; y < std::min(by + B, d.h); ++y)
                             for (uint32_t x = bx; x < std::min(bx + B, d.w); ++x) {
                                 const uint32_t o = d.out_off + y * d.w + x;
-                                pq.push_back(make_uint2(pm[o], o));
+                                const uint32_t fx = d.x0 + x, fy = d.y0 + y;
+                                const uint64_t key = rt_rng_pixel_key(c->sc.seed, fy * c->sc.width + fx);
+                                pq.push_back(make_uint4(pm[o], o, (uint32_t)key, (uint32_t)(key >> 32)));
                             }
             if (pix > c->d_pixmap_cap) {
                 if (c->d_pixmap) (void)hipFree(c->d_pixmap);
@@ -649,12 +652,12 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                 c->d_pixq = nullptr;
                 c->d_pixmap_cap = 0;
                 if (hipMalloc(&c->d_pixmap, pix * sizeof(uint32_t)) != hipSuccess ||
-                    hipMalloc(&c->d_pixq, pix * sizeof(uint2)) != hipSuccess)
+                    hipMalloc(&c->d_pixq, pix * sizeof(uint4)) != hipSuccess)
                     return set_err(c, RT_ERR_OOM, "pixel map alloc failed");
                 c->d_pixmap_cap = pix;
             }
             HIPCHK(c, hipMemcpy(c->d_pixmap, pm.data(), pix * sizeof(uint32_t), hipMemcpyHostToDevice));
-            HIPCHK(c, hipMemcpy(c->d_pixq, pq.data(), pix * sizeof(uint2), hipMemcpyHostToDevice));
+            HIPCHK(c, hipMemcpy(c->d_pixq, pq.data(), pix * sizeof(uint4), hipMemcpyHostToDevice));
         }
         c->pixmap_tiles = dt;
     }

@@ -139,10 +139,11 @@ struct LaunchArgs {
     uint32_t n_tiles;
     const uint32_t* pix_xy; // launch pixel o -> (y << 16) | x; nullptr for frames over 65535 wide/high
     // Queue order of the launch pixels (with pix_xy): the queue kernel's q-th pixel of a sample
-    // is {(y << 16) | x, o}, 8 x 8 blocks of each tile in turn, so a wave's consecutive items
-    // are a compact block of the frame (coherent camera rays for closest_packet).  nullptr:
-    // q = o.
-    const uint2* pix_q;
+    // is {(y << 16) | x, o, key}, 8 x 8 blocks of each tile in turn, so a wave's consecutive items
+    // are a compact block of the frame (coherent camera rays for closest_packet); key (low, high
+    // word) is the pixel's stream key rt_rng_pixel_key(seed, y * width + x), so a path start
+    // makes one SplitMix64 round instead of two.  nullptr: q = o.
+    const uint4* pix_q;
     uint32_t n_blocks;
     uint64_t sample_begin;
     uint32_t sample_count;

@@ -54,6 +54,9 @@
 #ifndef RT_PAIR_FETCH
 #define RT_PAIR_FETCH 1     // cooperative descent: a node's two children loaded together, before its decision (a380 +3%, biplane +3%)
 #endif
+#ifndef RT_PIX_KEY
+#define RT_PIX_KEY 1        // queue kernels: the pixel's stream key from the queue-order table (one SplitMix64 round per path start, not two)
+#endif
 #ifndef RT_PACKET
 #define RT_PACKET 1         // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
 #endif
@@ -1313,11 +1316,15 @@ __device__ __forceinline__ V3 cube_emissive(const DevScene& sc, V3 rd) {
 }
 
 // ---------------------------------------------------------------- camera (generate.rs:24-66)
-__device__ __forceinline__ Ray camera_ray(const DevScene& sc, int x, int y, rt_rng_state* rng) {
+// The pixel's base direction (cam_d + s_x right) + s_y up, before the lens and the jitter.
+__device__ __forceinline__ V3 camera_base_dir(const DevScene& sc, int x, int y) {
     V3 up = ld3(sc.cam_up), right = ld3(sc.right);
     float s_x = sc.x_cf * ((float)x - sc.x_off);
     float s_y = sc.y_cf * ((float)y - sc.y_off);
-    V3 d = (ld3(sc.cam_d) + s_x * right) + s_y * up;
+    return (ld3(sc.cam_d) + s_x * right) + s_y * up;
+}
+__device__ __forceinline__ Ray camera_ray(const DevScene& sc, V3 d, rt_rng_state* rng) {
+    V3 up = ld3(sc.cam_up), right = ld3(sc.right);
     Ray ray;
     if (sc.has_lens) {
         float a = sc.lens_r;
@@ -1560,10 +1567,10 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
 }
 
-__device__ __forceinline__ void start_path(const DevScene& sc, Path& p, int x, int y, uint32_t pix,
-                                           uint64_t s) {
-    p.rng = rt_rng_init(sc.seed, pix, s);
-    p.ray = camera_ray(sc, x, y, &p.rng);
+// key: the pixel's stream key, rt_rng_pixel_key(sc.seed, pixel) (rt_rng_init's first round)
+__device__ __forceinline__ void start_path(const DevScene& sc, Path& p, V3 dir, uint64_t key, uint64_t s) {
+    p.rng = rt_rng_init_key(key, s);
+    p.ray = camera_ray(sc, dir, &p.rng);
     p.L = mk(0.f, 0.f, 0.f);
     p.T = mk(1.f, 1.f, 1.f);
     p.depth = 0;
@@ -1609,7 +1616,9 @@ __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a
     if (K == 1 && a.sample_begin > 0) acc = xyz(a.accum[pix]);
     uint32_t i = 0;
     Path p;
-    if (n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk);
+    const uint64_t pkey = rt_rng_pixel_key(sc.seed, pix);
+    const V3 pdir = camera_base_dir(sc, x, y);
+    if (n_mine) start_path(sc, p, pdir, pkey, a.sample_begin + kk);
     while (i < n_mine) {
         if (segment<COUNT, GEN, DLS>(sc, p, st, c)) {
             const uint32_t rel = kk + K * i;
@@ -1623,7 +1632,7 @@ __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a
                 r[1] = p.L.y;
                 r[2] = p.L.z;
             }
-            if (++i < n_mine) start_path(sc, p, x, y, pix, a.sample_begin + kk + K * i);
+            if (++i < n_mine) start_path(sc, p, pdir, pkey, a.sample_begin + kk + K * i);
         }
     }
     if (COUNT) {
@@ -1773,15 +1782,22 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                     uint32_t j, o;
                     split_item(a, item, &j, &o);
                     int x, y;
+                    uint64_t key;
+                    V3 dir;
                     if (a.pix_q) {  // item j * n_pix + q: the q-th pixel in queue order
-                        const uint2 e = a.pix_q[o];
+                        const uint4 e = a.pix_q[o];
                         x = (int)(e.x & 0xffffu);
                         y = (int)(e.x >> 16);
                         o = e.y;
+                        key = RT_PIX_KEY ? ((uint64_t)e.w << 32) | e.z
+                                         : rt_rng_pixel_key(sc.seed, (uint32_t)y * sc.width + (uint32_t)x);
+                        dir = camera_base_dir(sc, x, y);
                     } else {
                         launch_pixel(a, o, &x, &y);
+                        key = rt_rng_pixel_key(sc.seed, (uint32_t)y * sc.width + (uint32_t)x);
+                        dir = camera_base_dir(sc, x, y);
                     }
-                    start_path(sc, p, x, y, (uint32_t)y * sc.width + (uint32_t)x, a.sample_begin + j);
+                    start_path(sc, p, dir, key, a.sample_begin + j);
                     slot = j * a.n_pix + o;
                     have = true;
                 } else {

@@ -47,9 +47,12 @@ RT_RNG_FN uint64_t rt_rng_mix64(uint64_t z) {
  * seed and pixel, sample -> state is a bijection (mix64 of a bijection of the sample), and the
  * pixel enters through the first mix, so no two (pixel, sample) pairs share a start unless the
  * 64-bit hashes collide. */
+RT_RNG_FN uint64_t rt_rng_pixel_key(uint64_t seed, uint32_t pixel) {
+    return rt_rng_mix64(seed + 0x9e3779b97f4a7c15ull * ((uint64_t)pixel + 1u));
+}
+RT_RNG_FN rt_rng_state rt_rng_init_key(uint64_t key, uint64_t sample) { return rt_rng_mix64(key ^ sample); }
 RT_RNG_FN rt_rng_state rt_rng_init(uint64_t seed, uint32_t pixel, uint64_t sample) {
-    const uint64_t k = rt_rng_mix64(seed + 0x9e3779b97f4a7c15ull * ((uint64_t)pixel + 1u));
-    return rt_rng_mix64(k ^ sample);
+    return rt_rng_init_key(rt_rng_pixel_key(seed, pixel), sample);
 }
 
 /* Next u32 of the stream (XSH-RR of the current state); advances *state. */
