@@ -103,3 +103,36 @@ def test_a380_batch1(gpu_available, oracle):
     s = parity.stats(g, o)
     print("a380 batch 1", s)
     assert np.array_equal(g, o), s
+
+
+# Whole frames, every pixel: the oracle's cost per sample (CPU column) makes a full
+# 1200 x 600 frame at 1-10 spp a few seconds of host work, so each benchmark scene is compared on
+# its entire frame, in the scheme's own batch size where that is smaller than the sample count.
+WHOLE = [
+    # scene, sample_begin, samples, batch, dir_light_samp
+    ("triangles", 0, 10, 10, 0),       # BASELINE config 0: 10 spp, depth 5
+    ("walled", 19000, 2, 2, 0),        # the bench's scene, late in its 20000-spp run
+    ("walled", 7, 1, 1, 1),            # direct-light sampling (radiance.rs:46-56,89-120)
+    ("biplane", 190, 2, 1, 0),         # config 3's tail, one-sample batches (pipelined launches)
+    ("spaceship_r1", 25, 1, 1, 0),
+    ("a380", 3, 2, 1, 0),              # config 2's batch of 1
+    ("spaceship_r1@4096", 0, 1, 1, 0),  # config 5's 4096 x 4096 frame (16.8 M pixels)
+]
+
+
+@pytest.mark.parametrize("name,s0,spp,batch,dls", WHOLE, ids=[f"{w[0]}-dls{w[4]}" for w in WHOLE])
+def test_whole_frame_bit_exact(gpu_available, oracle, name, s0, spp, batch, dls):
+    from rt_amd import render
+
+    scene, _, size = name.partition("@")
+    sc = load_scene(scene, **({"width": int(size), "height": int(size)} if size else {}))
+    sc.info.dir_light_samp = dls
+    w, h = int(sc.info.width), int(sc.info.height)
+    with render.Context(sc) as ctx:
+        for b in range(s0, s0 + spp, batch):
+            frame = ctx.render(None, b, batch, want_output=(b + batch == s0 + spp))
+    o = oracle.render(sc, [(0, 0, w, h)], s0, spp, accum=oracle.ACCUM_FORWARD)
+    s = parity.stats(frame, o)
+    print(f"{name} whole frame {w}x{h}, samples [{s0}, {s0 + spp}), dls {dls}", s)
+    assert (frame[:, 3] == 1.0).all()
+    assert np.array_equal(frame, o), s
