@@ -48,7 +48,7 @@ VALU_PEAK_WINST_S = 256 * 4 * 2.4e9 / 2
 BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits": 32, "mesh_hits": 132}
 
 
-from rt_amd.shard import STRIPE, max_rank_pixels, rank_tiles  # noqa: E402
+from rt_amd.shard import max_rank_pixels, rank_tiles, stripe_rows  # noqa: E402
 
 
 def reference_bytes_per_sample(ctx, width, height, spp=16, device=False):
@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--stripe", type=int, default=None,
+                    help="rows per stripe (default: rt_amd.shard.stripe_rows, equal stripe counts per rank)")
     ap.add_argument("--as-rank", default=None,
                     help="r/N: time rank r's share of an N-GPU run on this one GPU (no gather); "
                          "a scaling rehearsal, not the contract's multi-process run")
@@ -226,9 +228,10 @@ def main():
         if world != 1:
             raise SystemExit("--as-rank is a single-process rehearsal")
         shard_rank, shard_world = (int(v) for v in args.as_rank.split("/"))
-    tiles = rank_tiles(w, h, shard_rank, shard_world)
+    stripe = args.stripe or stripe_rows(h, shard_world)
+    tiles = rank_tiles(w, h, shard_rank, shard_world, stripe)
     npix = sum(t[2] * t[3] for t in tiles)
-    max_npix = max(max_rank_pixels(w, h, world), npix)
+    max_npix = max(max_rank_pixels(w, h, world, stripe), npix)
 
     ctx = render.Context(loaded, device=local)
     out = torch.zeros((max_npix, 4), dtype=torch.float32, device=f"cuda:{local}")
@@ -285,7 +288,7 @@ def main():
     if not args.as_rank and rank == 0:
         from rt_amd import shard
 
-        frame = shard.assemble(gather if dist else [out], w, h, world)
+        frame = shard.assemble(gather if dist else [out], w, h, world, stripe)
         frame_complete = bool((frame[..., 3] == 1.0).all().item())
 
     # every rank renders its pixels x spp_rank per step (weak: spp x N, strong: spp)
@@ -306,7 +309,7 @@ def main():
            "config": {"workload": f"{args.scene}.yml {w}x{h}, {spp} spp per step"
                                   f"{'' if args.strong else ' x n_gpus'} (one queue launch per rank and step), "
                                   f"kd_tree_depth {int(loaded.info.kd_tree_depth)}",
-                      "spp_per_step": spp, "pixels": w * h, "stripes": f"{STRIPE}-row round-robin",
+                      "spp_per_step": spp, "pixels": w * h, "stripes": f"{stripe}-row round-robin",
                       "parallelism": f"tiles{world}", "dispatch": "sync" if args.sync else "async"}}
     res["frame_complete"] = frame_complete
     res["launch"] = {"trace_launches_per_step": n_launch / args.steps, "samples_per_launch": round(per_launch),

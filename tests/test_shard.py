@@ -23,7 +23,18 @@ def test_stripes_partition_the_frame(w, h, world):
     assert (cover == 1).all()
     # balance: ranks differ by at most one stripe
     sizes = [shard.tile_pixels(shard.rank_tiles(w, h, r, world)) for r in range(world)]
-    assert max(sizes) - min(sizes) <= shard.STRIPE * w
+    stripe = shard.stripe_rows(h, world)
+    assert max(sizes) - min(sizes) <= stripe * w
+    if h % (stripe * world) == 0:
+        assert max(sizes) == min(sizes)
+
+
+def test_stripe_rows():
+    from rt_amd import shard
+
+    assert [shard.stripe_rows(600, n) for n in (1, 2, 4, 8)] == [8, 6, 6, 5]
+    assert [shard.stripe_rows(4096, n) for n in (1, 2, 4, 8)] == [8, 8, 8, 8]
+    assert shard.stripe_rows(37, 8) == 1
 
 
 def _pattern(w, h, tiles, n):
