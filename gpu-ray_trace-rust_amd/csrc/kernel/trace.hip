@@ -36,6 +36,9 @@
 #ifndef RT_REGEN_MIN
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 #endif
+#ifndef RT_REGEN_MIN_BATCH
+#define RT_REGEN_MIN_BATCH 1 // the sphere-only kernel with batched starts (RT_START_BATCH; lens scenes included): a start costs a few LDS reads, so idle lanes start at once (walled +6.3%; 4: +4.8%, 8: +3.5%)
+#endif
 #ifndef RT_REGEN_MIN_GEN
 #define RT_REGEN_MIN_GEN 16 // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
 #endif
@@ -56,6 +59,9 @@
 #endif
 #ifndef RT_PIX_KEY
 #define RT_PIX_KEY 1        // queue kernels: the pixel's stream key from the queue-order table (one SplitMix64 round per path start, not two)
+#endif
+#ifndef RT_START_BATCH
+#define RT_START_BATCH 1    // sphere-only queue kernel: camera rays made 64 at a time, at full wave width, and handed out from LDS
 #endif
 #ifndef RT_PACKET
 #define RT_PACKET 1         // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
@@ -1729,6 +1735,44 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
     return g < qmin ? qmin : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
+// Path starts in batches (RT_START_BATCH, the sphere-only kernel, cameras without a lens).  A
+// start is the item's pixel, the stream key, the SplitMix64 round and camera_ray's two jitter
+// draws.  Made by the idle lanes alone, it ran at the width of the lanes that had just finished,
+// so the wave waited for a dozen of them (RT_REGEN_MIN) while they idled through segments.
+// Instead the wave makes the camera rays of its next 64 items together, one per lane, and keeps
+// them in LDS (24 B: the unnormalized direction, the stream state after the draws, the radiance
+// slot); idle lanes take the next ones in order, at every segment.  A start is a pure function of
+// its item, so each item's path is the one start_path makes, bit for bit; only the lane that
+// traces it changes.  (A lens adds the origin to an entry: measured −0.7% from the extra
+// registers on walled, so lens scenes keep the per-lane starts.)
+constexpr uint32_t START_NONE = 0xffffffffu;  // slot of an entry past the launch's items
+constexpr int START_FIELDS = 6;
+__shared__ uint32_t g_start[BLOCK / 64][START_FIELDS][64];
+
+__device__ __forceinline__ void make_start(const LaunchArgs& a, const DevScene& sc, uint32_t item, uint32_t lane,
+                                           uint32_t (*e)[64]) {
+    uint32_t slot = START_NONE;
+    V3 d = mk(0.f, 0.f, 0.f);
+    rt_rng_state rng = 0;
+    if (item < a.n_items) {
+        uint32_t j, o;
+        split_item(a, item, &j, &o);
+        const uint4 q = a.pix_q[o];  // item j * n_pix + q: the q-th pixel in queue order
+        const int x = (int)(q.x & 0xffffu), y = (int)(q.x >> 16);
+        const uint64_t key = RT_PIX_KEY ? ((uint64_t)q.w << 32) | q.z
+                                        : rt_rng_pixel_key(sc.seed, (uint32_t)y * sc.width + (uint32_t)x);
+        rng = rt_rng_init_key(key, a.sample_begin + j);
+        d = camera_ray(sc, camera_base_dir(sc, x, y), &rng).d;  // no lens: the origin is cam_o
+        slot = j * a.n_pix + q.y;
+    }
+    e[0][lane] = __float_as_uint(d.x);
+    e[1][lane] = __float_as_uint(d.y);
+    e[2][lane] = __float_as_uint(d.z);
+    e[3][lane] = (uint32_t)rng;
+    e[4][lane] = (uint32_t)(rng >> 32);
+    e[5][lane] = slot;
+}
+
 template <bool GEN, bool DLS, bool RESTART, bool SLAB = false>
 __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a, const uint2* __restrict__ pk_nodes,
                                                                                 const uint32_t* __restrict__ pk_refs,
@@ -1752,6 +1796,9 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
+    // RT_START_BATCH: the wave's current batch of starts, entries [st_pos, 64) not yet taken
+    uint32_t st_pos = 64u, st_n = 0u;
+    const bool batch_ok = !GEN && !sc.has_lens && a.pix_q != nullptr;
 #if RT_TIMING
     // sphere-only kernel: wave clock in path starts, normalize, closest hit and shading
     unsigned long long tq_regen = 0, tq_norm = 0, tq_closest = 0, tq_shade = 0, tq_seg = 0;
@@ -1761,10 +1808,59 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         const unsigned long long tq0 = TM_NOW();
 #endif
         const uint64_t need = __ballot(!have && !done);
-        // Starting paths is wave-wide work at the width of the idle lanes: in the sphere-only
-        // kernel ~10 of 64 lanes end a path per segment, so it waits for RT_REGEN_MIN of them.
-        constexpr int regen_min = GEN ? RT_REGEN_MIN_GEN : RT_REGEN_MIN;
-        if (need && (regen_min <= 1 || __popcll(need) >= regen_min || __ballot(have) == 0)) {
+        // Starting paths is wave-wide work at the width of the idle lanes: ~10 of 64 lanes end a
+        // path per segment, so without batched starts the wave waits for RT_REGEN_MIN of them.
+        constexpr int regen_min = GEN ? RT_REGEN_MIN_GEN : (RT_START_BATCH ? RT_REGEN_MIN_BATCH : RT_REGEN_MIN);
+        const bool regen = need && (regen_min <= 1 || __popcll(need) >= regen_min || __ballot(have) == 0);
+        if (!GEN && RT_START_BATCH && regen && batch_ok) {
+            // the n idle lanes take entries st_pos .. st_pos + n - 1 of the batch, making the
+            // next batch (the wave's next 64 items) when it runs out
+            const uint32_t n = (uint32_t)__popcll(need);
+            const bool idle = !have && !done;
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            uint32_t (*e)[64] = g_start[threadIdx.x >> 6];
+            uint32_t v[START_FIELDS] = {0u, 0u, 0u, 0u, 0u, START_NONE};
+            auto take = [&](uint32_t ei) {
+#pragma unroll
+                for (int f = 0; f < START_FIELDS; ++f) v[f] = e[f][ei];
+            };
+            if (idle && r < st_n) take(st_pos + r);  // before the next batch overwrites them
+            if (n > st_n) {
+                if (pool == pool_end) {  // grabs are multiples of 64: a batch never spans two
+                    uint32_t b0 = 0;
+                    if (lane == 0) b0 = atomicAdd(a.queue, grab);
+                    pool = __builtin_amdgcn_readfirstlane(b0);
+                    pool_end = pool + grab;
+                    grab = grab_size<GEN>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+                }
+                __builtin_amdgcn_wave_barrier();
+                make_start(a, sc, pool + lane, lane, e);
+                pool += 64u;
+                __builtin_amdgcn_wave_barrier();
+                if (idle && r >= st_n) take(r - st_n);
+                st_pos = n - st_n;
+                st_n = 64u - st_pos;
+            } else {
+                st_pos += n;
+                st_n -= n;
+            }
+            if (idle) {
+                if (v[5] == START_NONE) {
+                    done = true;
+                } else {
+                    p.ray.o = ld3(sc.cam_o);
+                    p.ray.d = mk(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]));
+                    p.rng = ((uint64_t)v[4] << 32) | v[3];
+                    p.L = mk(0.f, 0.f, 0.f);
+                    p.T = mk(1.f, 1.f, 1.f);
+                    p.depth = 0;
+                    p.dls_on = false;
+                    slot = v[5];
+                    have = true;
+                }
+            }
+        } else if (regen) {
             const uint32_t n = (uint32_t)__popcll(need);
             const uint32_t left = pool_end - pool;
             uint32_t base = pool_end;

@@ -471,3 +471,26 @@ def test_packet_traversal_bit_invariant(gpu_available, monkeypatch, scene_name, 
     for cfg, got in imgs.items():
         for a, b in zip(got, ref):
             assert np.array_equal(a, b), (cfg, parity.stats(a, b))
+
+
+def test_sphere_scene_with_lens_bit_exact(gpu_available, oracle):
+    """walled.yml with its commented-out lens (`lens_r: 0.1`): the sphere-only kernel keeps the
+    per-lane path starts for lens cameras (RT_START_BATCH covers lens-free ones), and both render
+    the forward oracle's bits (generate.rs:24-66)."""
+    import json
+    import os
+
+    from conftest import SCENES
+    from rt_amd import render, scheme
+
+    d = json.load(open(os.path.join(SCENES, "walled.json")))
+    d["cam"]["lens_r"] = 0.1
+    sc = scheme.load(d)
+    assert sc.cam.has_lens == 1
+    crop = [(560, 260, 48, 24), (0, 0, 16, 16)]
+    with render.Context(sc) as ctx:
+        g = ctx.render(crop, 3, 8)
+    f = oracle.render(sc, crop, 3, 8, accum=oracle.ACCUM_FORWARD)
+    s = parity.stats(g, f)
+    print("walled with lens", s)
+    assert np.array_equal(g, f), s
