@@ -1,0 +1,59 @@
+"""The shipped library's gfx950 code object, read on the CPU: every kernel the runtime can
+launch has a real body.  A kernel the compiler reduced to `s_endpgm` (undefined behaviour, or a
+branch that made the work unreachable) renders nothing and returns success; the GPU parity tests
+catch that only for the scenes that reach it, so this checks every instantiation at build time.
+Format: the .hip_fatbin section is a clang offload bundle ("__CLANG_OFFLOAD_BUNDLE__", entry
+count, then offset / size / target triple per entry) holding an AMDGPU ELF per target."""
+import struct
+
+import pytest
+
+
+def _sections(b):
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx][4]
+    return {b[names + s[0]: b.index(b"\0", names + s[0])].decode(): s for s in secs}
+
+
+def _gfx950_object(lib_path):
+    b = open(lib_path, "rb").read()
+    s = _sections(b)[".hip_fatbin"]
+    fb = b[s[4]: s[4] + s[5]]
+    assert fb.startswith(b"__CLANG_OFFLOAD_BUNDLE__")
+    n, = struct.unpack_from("<Q", fb, 24)
+    off = 32
+    for _ in range(n):
+        o, size, tl = struct.unpack_from("<QQQ", fb, off)
+        triple = fb[off + 24: off + 24 + tl].decode()
+        off += 24 + tl
+        if triple.endswith("gfx950"):
+            return fb[o: o + size]
+    raise AssertionError("no gfx950 code object in the bundle")
+
+
+def _kernel_sizes(elf):
+    """{symbol: size in bytes} of the code object's functions (STT_FUNC)."""
+    secs = _sections(elf)
+    symtab, strtab = secs[".symtab"], secs[".strtab"]
+    out = {}
+    for i in range(symtab[5] // 24):
+        name_off, info, _other, _shndx, _value, size = struct.unpack_from("<IBBHQQ", elf, symtab[4] + 24 * i)
+        if info & 0xF == 2:  # STT_FUNC
+            out[elf[strtab[4] + name_off: elf.index(b"\0", strtab[4] + name_off)].decode()] = size
+    return out
+
+
+def test_every_kernel_has_a_body():
+    from rt_amd import abi
+
+    sizes = _kernel_sizes(_gfx950_object(abi.LIB_PATH))
+    queue = {k: v for k, v in sizes.items() if "queue_kernel" in k}
+    # queue_kernel<GEN, DLS, RESTART, SLAB>: sphere-only (stack / stackless), general (stack /
+    # stackless / LDS slabs), DLS (stack / stackless)
+    assert len(queue) == 7, sorted(queue)
+    for name, size in sorted(sizes.items()):
+        if "kernel" in name:
+            assert size > 256, f"{name}: {size} B of code (an empty kernel is 4)"
+    assert min(queue.values()) > 8192, queue
