@@ -3,21 +3,18 @@
 // reference's (Rust never contracts a*b+c).
 //
 // rt_kd_build restates KdTree::build / node_from_elems (src/accel/kdtree.rs:26-56,107-137)
-// iteratively (breadth first, the nodes of a level in parallel) into the 8-byte node layout of rt_abi.h, then re-lays the nodes
+// iteratively (breadth first) into the 8-byte node layout of rt_abi.h, then re-lays the nodes
 // in 128-byte blocks (relayout_blocked) for cache-line locality on the device.  The split of a node is the f32 sequential mean of its elements' AABB centroids on
 // the node's axis (Sum<Vector3<f32>> folds from zero in element order, kdtree.rs:113); an
 // element goes high when aabb.high >= split and low when aabb.low <= split (both allowed,
 // kdtree.rs:119-127); a node is a leaf when depth > max_depth or it holds <= 1 element.
 #include "host_internal.h"
 
-#include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <new>
-#include <thread>
 #include <vector>
 
 namespace rth {
@@ -173,97 +170,39 @@ extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd
             kt->pub.bounds[2 * a] = lo;
             kt->pub.bounds[2 * a + 1] = hi;
         }
-        // Level by level: the nodes of one level are independent (their splits and partitions
-        // read only their own elements), so they are computed in parallel; node numbering and
-        // the ref list are assigned in the sequential breadth-first order, so the tree is the
-        // single-threaded build's, node for node and ref for ref.  A level's element lists live
-        // in one flat array (an item is a range of it): pass 1 finds each node's split and the
-        // sizes of its two lists, a prefix over them places the lists in the next level's array,
-        // pass 2 writes them.  No per-node allocation.
-        struct Item { uint32_t node; size_t off; uint32_t cnt; };
-        struct Split { float split; uint32_t n_low, n_high; size_t low_off, high_off; };
-        std::vector<uint32_t> cur(std::move(root)), nxt;
-        std::vector<Item> level{Item{0, 0, (uint32_t)cur.size()}}, next_level;
-        std::vector<Split> res;
+        struct Item { uint32_t node; uint32_t depth; std::vector<uint32_t> elems; };
+        std::deque<Item> q;
         kt->nodes.push_back(rt_kd_node{0, 0});
-        const unsigned hw = std::thread::hardware_concurrency();
-        const unsigned max_threads = hw ? (hw < 16u ? hw : 16u) : 1u;
-        auto parallel_for = [&](size_t n, size_t work, auto&& f) {
-            const unsigned nt = (n > 1 && work >= 16384) ? (unsigned)std::min<size_t>(max_threads, n) : 1u;
-            if (nt <= 1) {
-                for (size_t i = 0; i < n; ++i) f(i);
-                return;
+        q.push_back(Item{0, 0, std::move(root)});
+        while (!q.empty()) {
+            Item it = std::move(q.front());
+            q.pop_front();
+            const uint32_t axis = it.depth % 3;
+            if (it.depth > max_depth || it.elems.size() <= 1) {
+                if (kt->refs.size() + it.elems.size() >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
+                kt->nodes[it.node].a = (uint32_t)it.elems.size();
+                kt->nodes[it.node].b = ((uint32_t)kt->refs.size() << 2) | RT_KD_LEAF;
+                kt->refs.insert(kt->refs.end(), it.elems.begin(), it.elems.end());
+                if (it.depth > max_leaf_depth) max_leaf_depth = it.depth;
+                continue;
             }
-            std::atomic<size_t> next{0};
-            auto run = [&]() {
-                for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);
-            };
-            std::vector<std::thread> pool;
-            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(run);
-            run();
-            for (std::thread& t : pool) t.join();
-        };
-        for (uint32_t depth = 0; !level.empty(); ++depth) {
-            const uint32_t axis = depth % 3;
-            const bool leaves = depth > max_depth;
-            res.assign(level.size(), Split{0.0f, 0u, 0u, 0u, 0u});
-            parallel_for(level.size(), cur.size(), [&](size_t i) {  // pass 1: split and list sizes
-                const Item& it = level[i];
-                if (leaves || it.cnt <= 1) return;
-                const uint32_t* el = cur.data() + it.off;
-                float sum = 0.0f;  // centroid component on `axis`, folded in element order
-                for (uint32_t k = 0; k < it.cnt; ++k) sum = sum + 0.5f * (rs[el[k]].lo[axis] + rs[el[k]].hi[axis]);
-                Split& r = res[i];
-                r.split = sum / (float)it.cnt;
-                for (uint32_t k = 0; k < it.cnt; ++k) {
-                    r.n_high += rs[el[k]].hi[axis] >= r.split ? 1u : 0u;
-                    r.n_low += rs[el[k]].lo[axis] <= r.split ? 1u : 0u;
-                }
-            });
-            // breadth-first order: leaves take their refs, inner nodes their children and the
-            // places of their two lists in the next level
-            size_t acc = 0;
-            next_level.clear();
-            for (size_t i = 0; i < level.size(); ++i) {
-                const Item& it = level[i];
-                if (leaves || it.cnt <= 1) {
-                    if (kt->refs.size() + it.cnt >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
-                    kt->nodes[it.node].a = it.cnt;
-                    kt->nodes[it.node].b = ((uint32_t)kt->refs.size() << 2) | RT_KD_LEAF;
-                    kt->refs.insert(kt->refs.end(), cur.begin() + it.off, cur.begin() + it.off + it.cnt);
-                    if (depth > max_leaf_depth) max_leaf_depth = depth;
-                    continue;
-                }
-                Split& r = res[i];
-                const uint32_t child = (uint32_t)kt->nodes.size();
-                if (child + 2 >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
-                std::memcpy(&kt->nodes[it.node].a, &r.split, 4);
-                kt->nodes[it.node].b = (child << 2) | axis;
-                kt->nodes.push_back(rt_kd_node{0, 0});
-                kt->nodes.push_back(rt_kd_node{0, 0});
-                r.low_off = acc;
-                acc += r.n_low;
-                r.high_off = acc;
-                acc += r.n_high;
-                next_level.push_back(Item{child, r.low_off, r.n_low});
-                next_level.push_back(Item{child + 1, r.high_off, r.n_high});
+            float sum = 0.0f;  // centroid component on `axis`, folded in element order
+            for (uint32_t e : it.elems) sum = sum + 0.5f * (rs[e].lo[axis] + rs[e].hi[axis]);
+            const float split = sum / (float)it.elems.size();
+            std::vector<uint32_t> low, high;
+            for (uint32_t e : it.elems) {
+                if (rs[e].hi[axis] >= split) high.push_back(e);
+                if (rs[e].lo[axis] <= split) low.push_back(e);
             }
-            nxt.resize(acc);
-            parallel_for(level.size(), cur.size(), [&](size_t i) {  // pass 2: the two lists, in element order
-                const Item& it = level[i];
-                if (leaves || it.cnt <= 1) return;
-                const Split& r = res[i];
-                const uint32_t* el = cur.data() + it.off;
-                uint32_t* lo = nxt.data() + r.low_off;
-                uint32_t* hi = nxt.data() + r.high_off;
-                for (uint32_t k = 0; k < it.cnt; ++k) {
-                    const uint32_t e = el[k];
-                    if (rs[e].hi[axis] >= r.split) *hi++ = e;
-                    if (rs[e].lo[axis] <= r.split) *lo++ = e;
-                }
-            });
-            cur.swap(nxt);
-            level.swap(next_level);
+            const uint32_t child = (uint32_t)kt->nodes.size();
+            if (child + 2 >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
+            std::memcpy(&kt->nodes[it.node].a, &split, 4);
+            kt->nodes[it.node].b = (child << 2) | axis;
+            kt->nodes.push_back(rt_kd_node{0, 0});
+            kt->nodes.push_back(rt_kd_node{0, 0});
+            std::vector<uint32_t>().swap(it.elems);
+            q.push_back(Item{child, it.depth + 1, std::move(low)});
+            q.push_back(Item{child + 1, it.depth + 1, std::move(high)});
         }
     }
     kt->nodes = relayout_blocked(kt->nodes);

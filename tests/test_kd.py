@@ -70,19 +70,3 @@ def test_single_and_empty_scenes(oracle):
     sc = scheme.load(one)
     kd = compare(sc, 17, oracle)
     assert len(kd.canonical_dfs()[0]) == 1 and kd.n_refs == 1
-
-
-def test_parallel_build_is_deterministic():
-    """rt_kd_build computes the nodes of a level on several threads; numbering and refs follow
-    the sequential breadth-first order, so repeated builds give the same bytes."""
-    import hashlib
-
-    from conftest import load_scene
-    from rt_amd import render
-
-    sc = load_scene("biplane")
-    digests = set()
-    for _ in range(3):
-        t = render.KdTree(sc.desc, int(sc.info.kd_tree_depth))
-        digests.add(hashlib.sha256(t.nodes.tobytes() + t.refs.tobytes()).hexdigest())
-    assert len(digests) == 1
