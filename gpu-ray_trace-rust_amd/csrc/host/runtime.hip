@@ -338,11 +338,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         texs[i] = DevTex{(uint32_t)texel_count, tx.width, tx.height, 0};
         texel_count += (uint64_t)tx.width * tx.height;
     }
-    std::vector<float> texels(3 * texel_count);
-    for (uint32_t i = 0; i < scene->n_textures; ++i) {
-        const rt_texture& tx = scene->textures[i];
-        std::memcpy(texels.data() + 3 * (size_t)texs[i].off, tx.rgb, 3 * sizeof(float) * tx.width * tx.height);
-    }
 
     DevScene& d = c->sc;
     std::memset(&d, 0, sizeof(d));
@@ -402,7 +397,17 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
     if ((st = upload(c, ftri_n, &d.ftri_n))) return st;
     if ((st = upload(c, ftri_mat, &d.ftri_mat))) return st;
-    if ((st = upload(c, texels, &d.texels))) return st;
+    if (texel_count) {  // each texture straight from the caller's array into the pool (no host staging copy)
+        void* p = nullptr;
+        if (hipMalloc(&p, 3 * sizeof(float) * texel_count) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
+        c->allocs.push_back(p);
+        for (uint32_t i = 0; i < scene->n_textures; ++i) {
+            const rt_texture& tx = scene->textures[i];
+            HIPCHK(c, hipMemcpy(static_cast<float*>(p) + 3 * (size_t)texs[i].off, tx.rgb,
+                                3 * sizeof(float) * (size_t)tx.width * tx.height, hipMemcpyHostToDevice));
+        }
+        d.texels = static_cast<const float*>(p);
+    }
     if ((st = upload(c, texs, &d.tex))) return st;
     if ((st = upload(c, mtri, &d.mtri))) return st;
     if ((st = upload(c, prims, &d.prims))) return st;
