@@ -37,7 +37,7 @@
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 #endif
 #ifndef RT_REGEN_MIN_BATCH
-#define RT_REGEN_MIN_BATCH 1 // the sphere-only kernel with batched starts (RT_START_BATCH; lens scenes included): a start costs a few LDS reads, so idle lanes start at once (walled +6.3%; 4: +4.8%, 8: +3.5%)
+#define RT_REGEN_MIN_BATCH 1 // the sphere-only kernel with batched starts (RT_START_BATCH): a start costs a few LDS reads, so idle lanes start at once (walled +6.5%; 4: +4.8%, 8: +3.5%); lens cameras, which keep per-lane starts, use it too
 #endif
 #ifndef RT_REGEN_MIN_GEN
 #define RT_REGEN_MIN_GEN 16 // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
