@@ -5,24 +5,34 @@ One step = one batch (the reference's gpu_render_batch, walled.yml: 1000 spp) ov
 pixels: rt_render_device_async, which overlaps step i + 1's trace with step i's drain tail
 (draw_scene.rs:30-44's batches are independent sample ranges; only their running-mean folds are
 ordered), plus — for N > 1 — the frame-end RCCL gather of every rank's tile radiance to rank 0,
-on torch's stream behind the step's fold.  Inputs (scene, KD tree) are resident in HBM before the
-timed region.  N GPUs: one process per GPU (torch.distributed.run), image rows dealt to ranks as
-1-row stripes.  Default weak scaling: at N GPUs a step renders N x spp samples for every pixel,
-so each rank keeps the 1-GPU step's work (W*H/N pixels x N*spp samples).  --strong keeps the
-frame fixed (W*H*spp per step over all ranks; BASELINE config 5 is spaceship_r1 4096^2 at 1000
-spp = `--scene spaceship_r1 --width 4096 --height 4096 --spp-per-step 25 --strong --steps 40`).
-Either way the image is bit-identical to the 1-GPU one (the RNG and the running mean are keyed
-on the global pixel and the absolute sample index).
+on torch's stream behind the step's fold (rt_amd/shard.py FrameSteps).  Inputs (scene, KD tree)
+are resident in HBM before the timed region.  N GPUs: one process per GPU
+(torch.distributed.run), image rows dealt to ranks as stripes of up to 8 rows, round-robin
+(rt_amd.shard.stripe_rows).
+
+Scaling: `value` is strong (fixed-frame) scaling — the N ranks split the W*H*spp samples of each
+step, as `north_star`'s tile-parallel split of one frame asks (draw_scene.rs:17-47) and BASELINE
+config 5 is (spaceship_r1 4096^2 at 1000 spp = `--scene spaceship_r1 --width 4096 --height 4096
+--spp-per-step 25 --steps 40`).  For N > 1 a weak-scaling run (each rank keeps the 1-GPU step's
+work: W*H/N pixels x N*spp) is reported beside it under "weak".  Either way the image is
+bit-identical to the 1-GPU one (RNG and running mean are keyed on the global pixel and the
+absolute sample index).
 
 Prints ONE JSON line (rank 0).  `roofline` names the measured limiter of the trace kernel:
 VALU issue (SQ_INSTS_VALU per launch over the launch's HIP-event duration, against 256 CUs x
-4 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz) unless HBM traffic (FETCH_SIZE x 2)
-is the larger fraction.  Counter values come from the committed rocprofv3 passes
-(profiles/*_counters.json) of the SAME kernel build — keyed on a hash of the library's device
-code, so a kernel change without a re-profile prints null instead of a stale figure.  SURVEY.md
-§8d's algorithmic bytes of the reference's traversal are reported apart (`reference_work`):
-the device skips most of that work exactly, so they are not a roofline.
-`cpu_baseline` is the oracle restatement of the reference CPU renderer on all host cores.
+4 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz), HBM traffic (FETCH_SIZE x 2) or the
+vector-memory return path (TD busy), whichever is the largest fraction.  Counter values come
+from the committed rocprofv3 passes (profiles/*_counters.json) of the SAME kernel build — keyed
+on a hash of the library's device code, so a kernel change without a re-profile prints null
+instead of a stale figure.  SURVEY.md §8d's algorithmic bytes of the reference's traversal are
+reported apart (`reference_work`): the device skips most of that work exactly, so
+they are not a roofline.  `cpu_baseline` is the oracle restatement of the reference CPU renderer
+on the host's cores at BASELINE.md §2's sample counts.
+
+At N = 1 the line also carries `configs`: BASELINE.json's other single-GPU configs, each timed by
+this run — a380 (10 spp in batches of 1), biplane (200 spp in batches of 10), spaceship_r1 at
+4096^2 (25-spp steps: one GPU's share of config 5), and triangles (config 0, 10 spp) — each with
+its own roofline and CPU baseline.
 """
 from __future__ import annotations
 
@@ -35,9 +45,18 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
-# rt_amd raises HIP's hardware queues per process (GPU_MAX_HW_QUEUES, before HIP starts) so that
-# the pipeline slots' streams overlap instead of sharing queues (launch pipeline)
-import rt_amd  # noqa: E402,F401
+
+# The launch pipeline's slots each want their own HIP hardware queue (launch
+# pipeline): this benchmark chooses GPU_MAX_HW_QUEUES = 12 before HIP starts unless the caller
+# asked for at least that, and reports what it ran with (rt_amd itself keeps explicit values).
+HW_QUEUES_BEFORE = os.environ.get("GPU_MAX_HW_QUEUES")
+try:
+    _q = int(HW_QUEUES_BEFORE or "0")
+except ValueError:
+    _q = 0
+if _q < 12:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+import rt_amd  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s chip-wide
@@ -46,9 +65,18 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s chip-wide
 VALU_PEAK_WINST_S = 256 * 4 * 2.4e9 / 2
 # Canonical per-event byte sizes of the reference algorithm's work
 BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits": 32, "mesh_hits": 132}
+# the CPU baseline's sample count per scene (steady-state per-sample throughput)
+CPU_SPP = {"walled": 20, "biplane": 10, "a380": 2, "spaceship_r1@4096": 1, "spaceship_r1": 2, "triangles": 10}
+# BASELINE.json configs timed beside the headline at N = 1: name -> (scene, total spp, batch,
+# width, height, timed repetitions of the whole config, warmup repetitions)
+CONFIGS = {
+    "a380": ("a380", 10, 1, None, None, 10, 1),                       # config 2: 10 spp, batch 1
+    "biplane": ("biplane", 200, 10, None, None, 2, 1),                # config 3: 200 spp, batch 10
+    "spaceship_r1@4096": ("spaceship_r1", 75, 25, 4096, 4096, 1, 1),  # config 5's per-GPU share: 3 steps of 25
+    "triangles": ("triangles", 10, 10, None, None, 20, 2),            # config 0: 10 spp
+}
 
-
-from rt_amd.shard import max_rank_pixels, rank_tiles, stripe_rows  # noqa: E402
+from rt_amd.shard import FrameSteps, rank_tiles, step_samples, stripe_rows  # noqa: E402
 
 
 def reference_bytes_per_sample(ctx, width, height, spp=16, device=False):
@@ -88,11 +116,21 @@ def measured_valu_stream():
     return None
 
 
-def roofline(scene, per_launch, kernel_ms, build_id, kernel):
+def min_insts(scene, build_id):
+    """The committed instruction floor of this kernel build on this scene (tools/min_insts.py)."""
+    p = os.path.join(ROOT, "profiles", f"min_insts_{scene}.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    return d, os.path.relpath(p, ROOT)
+
+
+def roofline(scene, per_launch, kernel_ms, build_id, kernel, kernel_ms_source):
     """Measured fractions of the trace kernel's ceilings; bound = the largest."""
     out = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-           "kernel": kernel, "kernel_ms_avg": round(kernel_ms, 3), "samples_per_launch": round(per_launch),
-           "build_id": build_id, "counters_source": None}
+           "kernel": kernel, "kernel_ms_avg": round(kernel_ms, 3), "kernel_ms_source": kernel_ms_source,
+           "samples_per_launch": round(per_launch), "build_id": build_id, "counters_source": None}
     c = committed_counters(build_id, scene, round(per_launch))
     if not c:
         out["note"] = "no committed rocprofv3 counters for this kernel build and workload: re-profile"
@@ -105,11 +143,22 @@ def roofline(scene, per_launch, kernel_ms, build_id, kernel):
         rate = d["valu_insts_per_launch"] / sec
         v = {"achieved": round(rate / 1e9, 1), "peak": round(VALU_PEAK_WINST_S / 1e9, 1),
              "unit": "G VALU wave-instructions/s", "frac": round(rate / VALU_PEAK_WINST_S, 4),
-             "insts_per_launch": d["valu_insts_per_launch"], "lane_util": d.get("valu_lane_util")}
+             "insts_per_launch": d["valu_insts_per_launch"], "lane_util": d.get("valu_lane_util"),
+             "wave_insts_per_sample": round(d["valu_insts_per_launch"] / per_launch, 2)}
         m = measured_valu_stream()
         if m:
             v["measured_fma_stream"] = m[0]
             v["frac_of_measured_stream"] = round(rate / 1e9 / m[0], 4)
+        mi = min_insts(scene, build_id)
+        if mi:
+            # the instruction floor bit-exactness fixes (lane-operations per sample, every lane
+            # busy) against the lane-slots the kernel actually issued per sample
+            floor = mi[0]["lane_ops_per_sample"]
+            issued = 64 * d["valu_insts_per_launch"] / per_launch
+            v["min_lane_ops_per_sample"] = floor
+            v["issued_lane_slots_per_sample"] = round(issued, 1)
+            v["min_insts_frac"] = round(floor / issued, 4)
+            v["min_insts_source"] = mi[1]
         out["valu"] = v
         fr["valu"] = v
     if d.get("hbm_read_bytes_per_launch"):
@@ -126,6 +175,8 @@ def roofline(scene, per_launch, kernel_ms, build_id, kernel):
         v = {"achieved": d["td_busy_frac"], "peak": 1.0, "unit": "fraction of cycles TD busy",
              "frac": d["td_busy_frac"], "ta_busy_frac": d.get("ta_busy_frac"),
              "note": "rocprofv3 TD_TD_BUSY_sum / 256 CUs over GRBM_GUI_ACTIVE / 8 XCDs, own pass"}
+        if d.get("vmem_rd_per_launch"):
+            v["vmem_wave_loads_per_sample"] = round(d["vmem_rd_per_launch"] / per_launch, 2)
         out["vmem"] = v
         fr["vmem"] = v
     if d.get("l2_bytes_per_launch"):
@@ -145,14 +196,27 @@ def roofline(scene, per_launch, kernel_ms, build_id, kernel):
     return out
 
 
-def cpu_baseline(loaded, target_s=15.0, threads=None):
-    """The oracle (C++ restatement of render_to_target_cpu, recursive radiance) on every host core
+def cgroup_cpus():
+    """CPU time the cgroup lets this process use, in CPUs (cpu.max quota / period), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(loaded, spp, threads=None):
+    """The oracle (C++ restatement of render_to_target_cpu, recursive radiance) over the full
+    frame at `spp` samples per pixel, one thread per CPU the process may run on
     (the reference's rayon par_iter_mut uses all of them, draw_scene.rs:73).  The KD build and
-    scene setup are timed apart (an oracle call with 0 samples), as SURVEY.md §8d asks."""
+    scene setup are timed apart (an oracle call with 0 samples), as SURVEY.md §8d asks.  `cores`
+    is the CPU time actually available: the thread count capped by the cgroup's CPU quota."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py  # test infrastructure: the CPU baseline leg only
 
-    threads = threads or os.cpu_count() or 1
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = threads or affinity
+    quota = cgroup_cpus()
     w, h = int(loaded.info.width), int(loaded.info.height)
     full = [(0, 0, w, h)]
 
@@ -163,8 +227,6 @@ def cpu_baseline(loaded, target_s=15.0, threads=None):
 
     timed(0)  # one-time loading
     t_build = min(timed(0), timed(0))
-    t1 = timed(1) - t_build
-    spp = max(1, min(1024, int(target_s / max(t1, 1e-3))))
     dt = timed(spp) - t_build
     model = "unknown"
     try:
@@ -174,10 +236,91 @@ def cpu_baseline(loaded, target_s=15.0, threads=None):
                 break
     except OSError:
         pass
-    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-            "kind": "port", "cpu_model": model, "host_cpus": os.cpu_count(), "kd_build_s": round(t_build, 3),
-            "sample": f"full {w}x{h} frame, {spp} spp in one call on {threads} threads ({dt:.1f} s after "
-                      f"the KD build); oracle/oracle.cpp recursive radiance"}
+    cores = min(threads, quota) if quota else threads
+    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "threads": threads, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "cpu_model": model,
+            "kd_build_s": round(t_build, 3),
+            "sample": f"full {w}x{h} frame, {spp} spp (BASELINE.md §2) in one call on {threads} threads "
+                      f"({dt:.1f} s after the KD build, CPU quota {quota or 'none'}); oracle/oracle.cpp "
+                      f"recursive radiance"}
+
+
+def kernel_label(loaded):
+    """The trace kernel the scene launches (trace.hip with_queue_kernel's defaults)."""
+    spheres_only = (loaded.desc.n_free_tris == 0 and loaded.desc.n_meshes == 0
+                    and loaded.desc.n_spheres <= 64 and not int(loaded.info.dir_light_samp))
+    dls = int(loaded.info.dir_light_samp) != 0
+    restart = spheres_only or os.environ.get("RT_KD_RESTART", "0") not in ("0", "")
+    slab = os.environ.get("RT_KD_RESTART") == "2"
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    return f"rtd::queue_kernel<{b(not spheres_only)}, {b(dls)}, {b(restart)}, {b(slab)}>"
+
+
+def load(scene, width=None, height=None):
+    from rt_amd import scheme
+
+    sch = scheme.load_json(os.path.join(ROOT, "tests", "golden", "scenes", scene + ".json"))
+    return sch, scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"), width=width, height=height)
+
+
+def sync_kernel_ms(ctx, tiles, sample, spp):
+    """One synchronous call of `spp` samples: the average trace launch alone (no neighbouring
+    launch overlapping it), for the roofline of pipelined (mesh) workloads."""
+    ctx.render(tiles, sample, spp, want_output=False)
+    ls = ctx.launch_stats()
+    return ls["trace_ms"] / max(ls["n_timed_launches"], 1)
+
+
+def run_config(name, cpu, build_id):
+    """One BASELINE.json config on this GPU: the whole config (its total spp in the scheme's
+    batches, async, pipelined) `reps` times after `warm` untimed runs; Msamples/s over the timed
+    runs, the roofline of its trace launches and the CPU baseline at BASELINE.md §2's spp."""
+    import torch
+
+    from rt_amd import render
+
+    scene, total, batch, width, height, reps, warm = CONFIGS[name]
+    _, loaded = load(scene, width, height)
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    tiles = [(0, 0, w, h)]
+    res = {"workload": f"{scene}.yml {w}x{h}, {total} spp in batches of {batch} "
+                       f"({total // batch} async calls), kd_tree_depth {int(loaded.info.kd_tree_depth)}"}
+    with render.Context(loaded) as ctx:
+        out = torch.zeros((w * h, 4), dtype=torch.float32, device="cuda:0")
+        stream = torch.cuda.current_stream().cuda_stream
+        sample = 0
+
+        def whole():
+            nonlocal sample
+            for _ in range(total // batch):
+                ctx.render_device_async(out.data_ptr(), tiles, sample, batch, stream=stream)
+                sample += batch
+
+        for _ in range(warm):
+            whole()
+        ctx.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            whole()
+        ctx.synchronize()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ls = ctx.launch_stats()
+        kms = sync_kernel_ms(ctx, tiles, sample, batch)
+        ok = bool((out[:, 3] == 1.0).all().item())
+    per_launch = w * h * batch
+    res.update(value=round(w * h * total * reps / elapsed / 1e6, 3), unit="Msamples/s", spp=total, batch=batch,
+               reps=reps, elapsed_s=round(elapsed, 4), frame_complete=ok,
+               launch={"trace_launches": ls["n_trace_launches"], "samples_per_launch": per_launch,
+                       "trace_ms_per_launch_overlapped": round(ls["trace_ms"] / max(ls["n_timed_launches"], 1), 3),
+                       "trace_ms_per_launch_sync": round(kms, 3)})
+    res["roofline"] = roofline(scene if name != "spaceship_r1@4096" else "spaceship_r1", per_launch, kms, build_id,
+                               kernel_label(loaded), "one synchronous launch (no overlap)")
+    if cpu:
+        res["cpu_baseline"] = cpu_baseline(loaded, CPU_SPP[name])
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    return res
 
 
 def main():
@@ -190,24 +333,31 @@ def main():
                     help="samples per pixel per step (default: the scheme's gpu_render_batch)")
     ap.add_argument("--width", type=int, default=None, help="override the scheme's width")
     ap.add_argument("--height", type=int, default=None, help="override the scheme's height")
-    ap.add_argument("--strong", action="store_true", help="fixed frame: N ranks split W*H*spp per step")
+    ap.add_argument("--weak", action="store_true", help="weak scaling as the headline (each rank N*spp)")
+    ap.add_argument("--strong", action="store_true", help="(the default) fixed frame: N ranks split W*H*spp")
     ap.add_argument("--sync", action="store_true", help="synchronous steps (rt_render_device), for A/B")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N = 1)")
     ap.add_argument("--stripe", type=int, default=None,
                     help="rows per stripe (default: rt_amd.shard.stripe_rows, equal stripe counts per rank)")
     ap.add_argument("--as-rank", default=None,
                     help="r/N: time rank r's share of an N-GPU run on this one GPU (no gather); "
                          "a scaling rehearsal, not the contract's multi-process run")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: gather host copies (multi-rank test with every rank on one GPU)")
+    ap.add_argument("--same-device", action="store_true", help="every rank on device 0 (tests; gloo only)")
+    ap.add_argument("--dump-frame", default=None, help="rank 0 saves the last assembled frame (.npy)")
     args = ap.parse_args()
+    if args.same_device and args.dist_backend != "gloo":
+        raise SystemExit("--same-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
@@ -215,12 +365,14 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
-    from rt_amd import abi, render, scheme
+    from rt_amd import abi, render
 
-    sch = scheme.load_json(os.path.join(ROOT, "tests", "golden", "scenes", args.scene + ".json"))
-    loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"), width=args.width, height=args.height)
+    sch, loaded = load(args.scene, args.width, args.height)
     w, h = int(loaded.info.width), int(loaded.info.height)
     spp = args.spp_per_step or int(sch["render_info"].get("gpu_render_batch") or 1)
     shard_rank, shard_world = rank, world
@@ -230,99 +382,70 @@ def main():
         shard_rank, shard_world = (int(v) for v in args.as_rank.split("/"))
     stripe = args.stripe or stripe_rows(h, shard_world)
     tiles = rank_tiles(w, h, shard_rank, shard_world, stripe)
-    npix = sum(t[2] * t[3] for t in tiles)
-    max_npix = max(max_rank_pixels(w, h, world, stripe), npix)
+    strong = not args.weak
 
     ctx = render.Context(loaded, device=local)
-    out = torch.zeros((max_npix, 4), dtype=torch.float32, device=f"cuda:{local}")
-    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
-    stream = torch.cuda.current_stream().cuda_stream
 
-    def barrier():
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
+    def timed_run(strong_mode):
+        spp_rank, job_samples = step_samples(w, h, spp, shard_world, strong_mode)
+        fs = FrameSteps(ctx, tiles, w, h, rank, world, stripe, spp_rank, local, dist=dist,
+                        backend=args.dist_backend, sync=args.sync)
+        r = fs.run(args.steps, args.warmup)
+        if args.as_rank:
+            job_samples = fs.npix * spp_rank  # one rank's share only
+        r.update(spp_rank=spp_rank, npix=fs.npix, value=job_samples * args.steps / r["elapsed_s"] / 1e6)
+        return fs, r
 
-    sample = 0
-    spp_rank = spp if args.strong else spp * shard_world  # weak: per-rank work is the 1-GPU step's
-    gather_ev = []
-
-    def step():
-        nonlocal sample
-        if args.sync:
-            ctx.render_device(out.data_ptr(), tiles, sample, spp_rank)
-        else:
-            ctx.render_device_async(out.data_ptr(), tiles, sample, spp_rank, stream=stream)
-        sample += spp_rank
-        if dist:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            dist.gather(out, gather_list=gather, dst=0)
-            e1.record()
-            gather_ev.append((e0, e1))
-
-    for _ in range(args.warmup):
-        step()
-    ctx.synchronize()
-    barrier()
-    gather_ev.clear()
-    sync_stats = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        if args.sync:
-            sync_stats.append(ctx.launch_stats())  # each synchronous call is its own window
-    ctx.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    # every trace launch of the timed steps (HIP events on their streams)
-    ls = ctx.launch_stats() if not args.sync else {
-        k: sum(s[k] for s in sync_stats) for k in ("render_ms", "trace_ms", "n_trace_launches")}
-    if dist:
-        t = torch.tensor([elapsed], device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    # after the timed region: rank 0 reassembles the last gathered frame (rt_amd/shard.py) and
-    # checks that every pixel was rendered by some rank (alpha is 1 exactly where written)
+    fs, r = timed_run(strong)
+    elapsed, ls, spp_rank, npix = r["elapsed_s"], r["launch"], r["spp_rank"], r["npix"]
+    # after the timed region: rank 0 reassembles the last gathered frame and checks that every
+    # pixel was rendered by some rank (alpha is 1 exactly where written)
     frame_complete = None
     if not args.as_rank and rank == 0:
-        from rt_amd import shard
+        frame = fs.frame()
+        frame_complete = bool((frame[..., 3] == 1.0).all())
+        if args.dump_frame:
+            import numpy as np
 
-        frame = shard.assemble(gather if dist else [out], w, h, world, stripe)
-        frame_complete = bool((frame[..., 3] == 1.0).all().item())
+            np.save(args.dump_frame, frame)
+    del fs
 
-    # every rank renders its pixels x spp_rank per step (weak: spp x N, strong: spp)
-    total_samples = (npix if args.as_rank else w * h) * spp_rank * args.steps
-    value = total_samples / elapsed / 1e6
     n_launch = ls["n_trace_launches"]
     per_launch = npix * spp_rank * args.steps / max(n_launch, 1)
-    kernel_ms = ls["trace_ms"] / max(n_launch, 1)
-    spheres_only = loaded.desc.n_free_tris == 0 and loaded.desc.n_meshes == 0
-    kernel = (f"rtd::queue_kernel<{'false' if spheres_only else 'true'}, "
-              f"{'true' if int(loaded.info.dir_light_samp) else 'false'}>")
+    kernel_ms = ls["trace_ms"] / max(ls.get("n_timed_launches", n_launch), 1)
     res = {"metric": f"Msamples/s (pixels x spp / s) on {args.scene}.yml",
-           "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+           "value": round(r["value"], 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-           "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None,
+           "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
            "dtype": "f32",
            "data": "synthetic-free: the reference's own scene file (tests/golden/scenes), seeded RNG",
            "config": {"workload": f"{args.scene}.yml {w}x{h}, {spp} spp per step"
-                                  f"{'' if args.strong else ' x n_gpus'} (one queue launch per rank and step), "
+                                  f"{'' if strong else ' x n_gpus'} (one queue launch per rank and step), "
                                   f"kd_tree_depth {int(loaded.info.kd_tree_depth)}",
                       "spp_per_step": spp, "pixels": w * h, "stripes": f"{stripe}-row round-robin",
-                      "parallelism": f"tiles{world}", "dispatch": "sync" if args.sync else "async"}}
+                      "parallelism": f"tiles{world}", "dispatch": "sync" if args.sync else "async",
+                      "dist_backend": args.dist_backend if world > 1 else None}}
     res["frame_complete"] = frame_complete
     res["launch"] = {"trace_launches_per_step": n_launch / args.steps, "samples_per_launch": round(per_launch),
                      "trace_ms_per_launch": round(kernel_ms, 3),
                      "device_window_ms": round(ls["render_ms"], 3)}
-    if gather_ev:
-        res["gather_ms_per_step"] = round(sum(a.elapsed_time(b) for a, b in gather_ev) / len(gather_ev), 3)
+    res["hw_queues"] = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "caller_value": HW_QUEUES_BEFORE,
+                        "hip_started_before_rt_amd": rt_amd.hw_queues()["hip_started_before_import"]}
+    if "gather_ms_per_step" in r:
+        res["gather_ms_per_step"] = round(r["gather_ms_per_step"], 3)
     if args.as_rank:
         res["config"]["rehearsal"] = f"rank {shard_rank} of {shard_world}, single GPU, no gather"
         res["scaling"] = None
+    if world > 1:  # weak scaling beside the strong headline (each rank keeps the 1-GPU step's work)
+        _, rw = timed_run(not strong)
+        res["weak" if strong else "strong"] = {
+            "value": round(rw["value"], 3), "ms_per_step": round(rw["elapsed_s"] / args.steps * 1e3, 3),
+            "spp_per_rank_step": rw["spp_rank"], "gather_ms_per_step": round(rw.get("gather_ms_per_step", 0.0), 3)}
 
+    build_id = abi.kernel_build_id()
     if rank == 0 and not args.no_roofline:
-        res["roofline"] = roofline(args.scene, per_launch, kernel_ms, abi.kernel_build_id(), kernel)
+        res["roofline"] = roofline(args.scene, per_launch, kernel_ms, build_id, kernel_label(loaded),
+                                   "HIP events around each trace launch of the timed steps")
         bps, counts = reference_bytes_per_sample(ctx, w, h)
         dev_bps, dev_counts = reference_bytes_per_sample(ctx, w, h, device=True)
         res["reference_work"] = {
@@ -335,9 +458,16 @@ def main():
             "note": "SURVEY.md §8d canonical bytes of the REFERENCE algorithm's work (rt_count_work), priced "
                     "per launch over the launch's duration: not a roofline, the device skips most of this "
                     "work exactly (closest_small, DESIGN.md §5)"}
-    if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(loaded, args.cpu_seconds, args.cpu_threads)
     ctx.close()
+    single = rank == 0 and world == 1 and not args.as_rank
+    if single and not args.no_cpu:
+        cs = CPU_SPP.get(args.scene if not (args.width or args.height) else args.scene + f"@{w}", 2)
+        res["cpu_baseline"] = cpu_baseline(loaded, cs, args.cpu_threads)
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    if single and not args.no_configs and args.scene == "walled":
+        res["configs"] = {}
+        for name in CONFIGS:
+            res["configs"][name] = run_config(name, not args.no_cpu, build_id)
     if dist:
         dist.destroy_process_group()
     if rank == 0:

@@ -66,8 +66,12 @@ struct rt_ctx {
     // Timing window: every trace launch since the window opened, as start / stop event pairs,
     // and the whole window from its first launch to its last fold (closed by rt_synchronize
     // or at the end of a synchronous call).
+    // Per-launch events are kept for the first MAX_TIMED_LAUNCHES launches of a window only, so
+    // a caller that never calls rt_synchronize (it syncs through its own stream) does not grow
+    // the pool without bound; later launches are counted but not timed.
     std::vector<hipEvent_t> lev;
-    uint32_t n_launch = 0;
+    uint32_t n_launch = 0;            // trace launches in the window
+    uint32_t n_timed = 0;             // ... of which timed (lev[2i], lev[2i + 1])
     hipEvent_t win_end = nullptr;     // the window's last event (win_end_ev or a launch stop)
     hipEvent_t win_end_ev = nullptr;
     bool pending = false;             // enqueued work not yet synchronised
@@ -75,6 +79,7 @@ struct rt_ctx {
     DevScene sc{};
     std::vector<void*> allocs;
     float4* accum = nullptr;
+    float4* accum_range = nullptr;    // rt_render_range's per-call mean (allocated on first use)
     DevTile* d_tiles = nullptr;
     uint32_t d_tiles_cap = 0;
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
@@ -169,6 +174,7 @@ static void destroy_ctx(rt_ctx* c) {
     for (Slot& sl : c->slot) if (sl.stream) (void)hipStreamSynchronize(sl.stream);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->accum) (void)hipFree(c->accum);
+    if (c->accum_range) (void)hipFree(c->accum_range);
     if (c->d_tiles) (void)hipFree(c->d_tiles);
     if (c->d_pixmap) (void)hipFree(c->d_pixmap);
     if (c->d_pixq) (void)hipFree(c->d_pixq);
@@ -239,7 +245,11 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         std::vector<uint32_t> packed;
         packed.reserve(refs.size() / 4);
         for (uint2& n : nodes) {
-            if ((n.y & 3u) != RT_KD_LEAF || n.x == 0) continue;
+            if ((n.y & 3u) != RT_KD_LEAF) continue;
+            if (n.x == 0) {  // an empty leaf points at the start of the packed list: its old
+                n.y = RT_KD_LEAF;  // offset may lie past the end of it (no read needs it anyway)
+                continue;
+            }
             const uint32_t off = n.y >> 2;
             std::string key(reinterpret_cast<const char*>(refs.data() + off), 4 * (size_t)n.x);
             auto it = seen.find(key);
@@ -561,13 +571,13 @@ static int sync_all(rt_ctx* c) {
     if (!c->pending) return RT_OK;
     c->pending = false;
     c->trace_ms = 0.f;
-    for (uint32_t i = 0; i < c->n_launch; ++i) {
+    for (uint32_t i = 0; i < c->n_timed; ++i) {
         float ms = 0.f;
         HIPCHK(c, hipEventElapsedTime(&ms, c->lev[2 * i], c->lev[2 * i + 1]));
         c->trace_ms += ms;
     }
     c->last_ms = 0.f;
-    if (c->n_launch && c->win_end) HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->lev[0], c->win_end));
+    if (c->n_timed && c->win_end) HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->lev[0], c->win_end));
     return RT_OK;
 }
 
@@ -576,12 +586,26 @@ static void open_window(rt_ctx* c) {
     if (c->pending) return;
     c->pending = true;
     c->n_launch = 0;
+    c->n_timed = 0;
     c->win_end = nullptr;
 }
 
-// An event from the pool: launch i's start (begin) or stop, recorded on `s`.
+// An event from the pool: launch i's start (begin) or stop, recorded on `s`.  Past
+// MAX_TIMED_LAUNCHES launches in one window nothing is recorded, except a stop that must end
+// the window (`out`), which goes to win_end_ev.
+static constexpr uint32_t MAX_TIMED_LAUNCHES = 256;
 static int record_launch_event(rt_ctx* c, bool begin, hipStream_t s, hipEvent_t* out = nullptr) {
-    const size_t i = 2 * (size_t)c->n_launch + (begin ? 0 : 1);
+    if (c->n_timed >= MAX_TIMED_LAUNCHES) {
+        if (!begin) {
+            c->n_launch++;
+            if (out) {
+                HIPCHK(c, hipEventRecord(c->win_end_ev, s));
+                *out = c->win_end_ev;
+            }
+        }
+        return RT_OK;
+    }
+    const size_t i = 2 * (size_t)c->n_timed + (begin ? 0 : 1);
     while (c->lev.size() <= i) {
         hipEvent_t e;
         HIPCHK(c, hipEventCreate(&e));
@@ -589,7 +613,10 @@ static int record_launch_event(rt_ctx* c, bool begin, hipStream_t s, hipEvent_t*
     }
     HIPCHK(c, hipEventRecord(c->lev[i], s));
     if (out) *out = c->lev[i];
-    if (!begin) c->n_launch++;
+    if (!begin) {
+        c->n_launch++;
+        c->n_timed++;
+    }
     return RT_OK;
 }
 
@@ -834,15 +861,26 @@ static int run_direct(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint32_t K, uint6
     return RT_OK;
 }
 
-// Enqueues one rt_render* call.  `after`: an event the output writers must wait for.
+// Enqueues one rt_render* call.  `after`: an event the output writers must wait for.  `range`:
+// the mean over this call's samples alone (rt_render_range), in accum_range.
 static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
-                       uint32_t sample_count, float4* dev_out, hipEvent_t after) {
+                       uint32_t sample_count, float4* dev_out, hipEvent_t after, bool range = false) {
     LaunchArgs a{};
     uint64_t n_out = 0;
     const uint32_t K = choose_k(c, tile_pixels(tiles, n_tiles));
     int st = prepare_tiles(c, tiles, n_tiles, use_queue(c) ? 1 : K, &a, &n_out);
     if (st) return st;
     a.out = dev_out;
+    if (range) {
+        if (!c->accum_range) {
+            st = sync_all(c);
+            if (st) return st;
+            if (hipMalloc(&c->accum_range, (size_t)c->sc.width * c->sc.height * sizeof(float4)) != hipSuccess)
+                return set_err(c, RT_ERR_OOM, "range accumulator alloc failed");
+        }
+        a.accum = c->accum_range;
+        a.mean_base = sample_begin;
+    }
     if (!use_queue(c)) return run_direct(c, a, n_out, K, sample_begin, sample_count);
     open_window(c);
     return enqueue_queue(c, a, n_out, sample_begin, sample_count, after);
@@ -872,6 +910,23 @@ extern "C" int rt_render(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
     if (out_rgba)  // on the stream of the last fold
         HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost,
                                  c->slot[c->cur_slot].stream));
+    return sync_all(c);
+}
+
+// The mean over [sample_begin, sample_begin + sample_count) alone: block_and_get_single_result
+// (gpu_utils.rs:681-724) of one batch, whose kernel folds its samples with a running mean that
+// starts at zero (trace.wgsl:277-318).  The context's cumulative mean is left alone.
+extern "C" int rt_render_range(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                               uint32_t sample_count, float* out_rgba) {
+    if (!c || !tiles || !out_rgba) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t n = tile_pixels(tiles, n_tiles);
+    int st;
+    if ((st = ensure_out(c, n))) return st;
+    if ((st = sync_all(c))) return st;
+    if ((st = render_impl(c, tiles, n_tiles, sample_begin, sample_count, c->d_out, nullptr, true))) return st;
+    HIPCHK(c, hipMemcpyAsync(out_rgba, c->d_out, n * sizeof(float4), hipMemcpyDeviceToHost,
+                             c->slot[c->cur_slot].stream));
     return sync_all(c);
 }
 
@@ -923,7 +978,7 @@ extern "C" int rt_last_launch_stats(const rt_ctx* c, rt_launch_stats* out) {
     out->render_ms = c->last_ms;
     out->trace_ms = c->trace_ms;
     out->n_trace_launches = c->n_launch;
-    out->_pad0 = 0;
+    out->n_timed_launches = c->n_timed;
     return RT_OK;
 }
 

@@ -147,6 +147,9 @@ struct LaunchArgs {
     uint32_t n_blocks;
     uint64_t sample_begin;
     uint32_t sample_count;
+    // The running mean's n for absolute sample s is s - mean_base: 0 for rt_render's cumulative
+    // mean (draw_scene.rs:81-83), the call's first sample for rt_render_range's per-call mean.
+    uint64_t mean_base;
     float4* accum;          // width*height running means
     float4* out;            // tile-concatenated output (may alias nothing)
     DevCounts* counts;      // instrumented launch only

@@ -1131,10 +1131,19 @@ __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax,
         float ll = 0.f, lu = 0.f, lv = 0.f;
         uint32_t lref = 0;
         // software pipeline: during the test of ref j, the primitive of ref j + 1 and the ref
-        // j + 2 are in flight (uploads carry zero padding past the end of refs)
-        uint32_t ref_n = ps.refs[off], ref_nn = ps.refs[off + 1];
-        const float4* pn = ps.prim4 + 3 * (size_t)(ref_n & REF_INDEX_MASK);
-        float4 b0 = pn[0], b1 = pn[1], b2 = pn[2];
+        // j + 2 are in flight (uploads carry zero padding past the end of refs).  An empty leaf
+        // reads nothing (cnt is wave-uniform: the node is).
+        uint32_t ref_n = 0, ref_nn = 0;
+        const float4* pn = ps.prim4;
+        float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, b2 = b0;
+        if (cnt) {
+            ref_n = ps.refs[off];
+            ref_nn = ps.refs[off + 1];
+            pn = ps.prim4 + 3 * (size_t)(ref_n & REF_INDEX_MASK);
+            b0 = pn[0];
+            b1 = pn[1];
+            b2 = pn[2];
+        }
         for (uint32_t j = 0; j < cnt; ++j) {
             const uint32_t ref = ref_n;
             const float4 a0 = b0, a1 = b1, a2 = b2;
@@ -1619,7 +1628,7 @@ __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a
     // this lane's samples: sample_begin + kk + K*j, j < n_mine
     const uint32_t n_mine = kk < a.sample_count ? (a.sample_count - kk + K - 1) / K : 0;
     V3 acc = mk(0.f, 0.f, 0.f);
-    if (K == 1 && a.sample_begin > 0) acc = xyz(a.accum[pix]);
+    if (K == 1 && a.sample_begin > a.mean_base) acc = xyz(a.accum[pix]);
     uint32_t i = 0;
     Path p;
     const uint64_t pkey = rt_rng_pixel_key(sc.seed, pix);
@@ -1629,7 +1638,7 @@ __global__ __launch_bounds__(BLOCK, RT_MIN_WAVES) void trace_kernel(LaunchArgs a
         if (segment<COUNT, GEN, DLS>(sc, p, st, c)) {
             const uint32_t rel = kk + K * i;
             if (K == 1) {
-                const float n = (float)(a.sample_begin + rel);  // running mean, draw_scene.rs:81-83
+                const float n = (float)(a.sample_begin - a.mean_base + rel);  // running mean, draw_scene.rs:81-83
                 acc = mk((p.L.x + (acc.x * n)) / (n + 1.0f), (p.L.y + (acc.y * n)) / (n + 1.0f),
                          (p.L.z + (acc.z * n)) / (n + 1.0f));
             } else if (!COUNT) {
@@ -1977,7 +1986,8 @@ __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
     launch_pixel(a, o, &x, &y);
     const uint32_t pix = (uint32_t)y * a.sc.width + (uint32_t)x;
     V3 acc = mk(0.f, 0.f, 0.f);
-    if (a.sample_begin > 0) acc = xyz(a.accum[pix]);
+    const uint64_t n0 = a.sample_begin - a.mean_base;  // the running mean's n of the first sample
+    if (n0 > 0) acc = xyz(a.accum[pix]);
     // (r + acc n) / (n + 1) per channel, in sample order; div3 is the division bit for bit
     // (exact reciprocal + Markstein quotients under their range guard).  The samples' loads are
     // issued FOLD_U at a time ahead of the sequential fold: with few launch pixels (a rank's
@@ -1998,13 +2008,13 @@ __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
         }
 #pragma unroll
         for (uint32_t u = 0; u < FOLD_U; ++u) {
-            const float n = (float)(a.sample_begin + j + u);
+            const float n = (float)(n0 + j + u);
             acc = div3(mk(v[3 * u] + (acc.x * n), v[3 * u + 1] + (acc.y * n), v[3 * u + 2] + (acc.z * n)), n + 1.0f);
         }
     }
     for (; j < a.sample_count; ++j) {
         const float* r = a.radiance + 3 * ((size_t)j * a.n_pix + o);
-        const float n = (float)(a.sample_begin + j);
+        const float n = (float)(n0 + j);
         acc = div3(mk(r[0] + (acc.x * n), r[1] + (acc.y * n), r[2] + (acc.z * n)), n + 1.0f);
     }
     const float4 ov = make_float4(acc.x, acc.y, acc.z, 1.0f);

@@ -108,7 +108,7 @@ class rt_kd_tree(C.Structure):
 
 class rt_launch_stats(C.Structure):
     _fields_ = [("render_ms", C.c_float), ("trace_ms", C.c_float), ("n_trace_launches", C.c_uint32),
-                ("_pad0", C.c_uint32)]
+                ("n_timed_launches", C.c_uint32)]
 
 
 class rt_work_counts(C.Structure):
@@ -141,6 +141,7 @@ EXPORTS = {
                                    C.c_void_p]),
     "rt_render_device_async": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
+    "rt_render_range": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32, P_f]),
     "rt_synchronize": (C.c_int, [C.c_void_p]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P_f]),
     "rt_last_launch_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_launch_stats)]),

@@ -38,6 +38,22 @@ class KdTree:
         self.unconditional = (np.ctypeslib.as_array(t.unconditional, shape=(t.n_unconditional,)).copy()
                               if t.n_unconditional else np.zeros(0, np.uint32))
 
+    def as_struct(self, nodes=None, refs=None) -> "abi.rt_kd_tree":
+        """This tree (or the same tree with `nodes` / `refs` replaced) as an rt_kd_tree for
+        rt_create; the numpy arrays it points into are kept on the returned struct."""
+        nodes = np.ascontiguousarray(self.nodes if nodes is None else nodes, dtype=np.uint32)
+        refs = np.ascontiguousarray(self.refs if refs is None else refs, dtype=np.uint32)
+        unc = np.ascontiguousarray(self.unconditional, dtype=np.uint32)
+        t = abi.rt_kd_tree()
+        t.n_nodes, t.n_refs = len(nodes), len(refs)
+        t.max_leaf_depth, t.n_unconditional = self.max_leaf_depth, len(unc)
+        t.bounds = (C.c_float * 6)(*self.bounds.tolist())
+        t.nodes = nodes.ctypes.data_as(C.POINTER(abi.rt_kd_node))
+        t.refs = refs.ctypes.data_as(abi.P_u32)
+        t.unconditional = unc.ctypes.data_as(abi.P_u32)
+        t._keep = (nodes, refs, unc)
+        return t
+
     def canonical_dfs(self):
         """Depth-first pre-order rows {is_leaf, axis, split bits | count, first ref} + refs —
         the same dump oracle_kd_dump produces from its pointer tree."""
@@ -74,12 +90,14 @@ class KdTree:
 class Context:
     """One rt_ctx on one gfx950 device (rt_create / rt_render / rt_destroy)."""
 
-    def __init__(self, loaded: LoadedScheme, device: int = 0, lib=None):
+    def __init__(self, loaded: LoadedScheme, device: int = 0, lib=None, tree: "abi.rt_kd_tree | None" = None):
+        """`tree`: a caller-supplied flattened KD tree (rt_kd_tree; NULL: rt_create builds one
+        with the scheme's kd_tree_depth)."""
         self.lib = lib or abi.load_library()
         self.loaded = loaded
         self.ctx = C.c_void_p()
-        st = self.lib.rt_create(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info), None,
-                                int(device), C.byref(self.ctx))
+        st = self.lib.rt_create(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info),
+                                C.byref(tree) if tree is not None else None, int(device), C.byref(self.ctx))
         abi.check(self.lib, st)
 
     @property
@@ -101,6 +119,16 @@ class Context:
         ptr = out.ctypes.data_as(abi.P_f) if want_output else None
         abi.check(self.lib, self.lib.rt_render(self.ctx, arr, n, int(sample_begin), int(sample_count), ptr),
                   self.ctx)
+        return out
+
+    def render_range(self, tiles=None, sample_begin: int = 0, sample_count: int = 1) -> np.ndarray:
+        """The mean over [sample_begin, sample_begin + sample_count) alone (rt_render_range): one
+        batch's result of the reference's GPU path (gpu_utils.rs:681-724)."""
+        tiles = tiles or self.full_tile()
+        arr, n = tiles_array(tiles)
+        out = np.empty((tile_pixels(tiles), 4), dtype=np.float32)
+        abi.check(self.lib, self.lib.rt_render_range(self.ctx, arr, n, int(sample_begin), int(sample_count),
+                                                     out.ctypes.data_as(abi.P_f)), self.ctx)
         return out
 
     def render_device(self, dev_ptr: int, tiles=None, sample_begin: int = 0, sample_count: int = 1):
@@ -128,11 +156,12 @@ class Context:
         return float(ms.value)
 
     def launch_stats(self) -> dict:
-        """{render_ms, trace_ms, n_trace_launches} of the last render call."""
+        """{render_ms, trace_ms, n_trace_launches, n_timed_launches} of the last render call
+        (trace_ms sums the n_timed_launches first launches of the window)."""
         st = abi.rt_launch_stats()
         abi.check(self.lib, self.lib.rt_last_launch_stats(self.ctx, C.byref(st)), self.ctx)
         return {"render_ms": float(st.render_ms), "trace_ms": float(st.trace_ms),
-                "n_trace_launches": int(st.n_trace_launches)}
+                "n_trace_launches": int(st.n_trace_launches), "n_timed_launches": int(st.n_timed_launches)}
 
     def count_work(self, tiles=None, sample_begin: int = 0, sample_count: int = 1, device: bool = False) -> dict:
         """Work counters: the reference algorithm's (default) or the device path's own."""

@@ -71,3 +71,118 @@ def gather_frame(buf, width: int, height: int, rank: int, world: int, dist, gath
         gather_list = [buf.new_empty(buf.shape) for _ in range(world)]
     dist.gather(buf, gather_list=gather_list if rank == 0 else None, dst=0)
     return assemble(gather_list, width, height, world) if rank == 0 else None
+
+
+def step_samples(width: int, height: int, spp: int, world: int, strong: bool) -> tuple:
+    """Sample accounting of one multi-rank step (bench.py): (spp every rank renders for each of
+    its pixels, samples all ranks render together).  Strong scaling keeps the frame fixed: the
+    ranks split W*H pixels at spp, so the job is W*H*spp whatever N.  Weak scaling keeps each
+    rank's work at the 1-GPU step's: W*H/N pixels at N*spp, so the job grows to W*H*N*spp."""
+    spp_rank = spp if strong else spp * world
+    return spp_rank, width * height * spp_rank
+
+
+class FrameSteps:
+    """The step loop of a sharded frame, as bench.py times it and the multi-rank
+    tests run it: each step renders `spp_rank` more samples of this rank's stripes into one device
+    buffer (rt_render_device_async on torch's current stream, or the synchronous rt_render_device),
+    then gathers every rank's buffer to rank 0 — the one collective per step.  backend "nccl"
+    (RCCL over xGMI) gathers the device buffers on torch's stream behind the step's fold; "gloo"
+    gathers host copies (several ranks sharing one GPU, where RCCL refuses)."""
+
+    def __init__(self, ctx, tiles, width: int, height: int, rank: int, world: int, stripe: int,
+                 spp_rank: int, device: int, dist=None, backend: str = "nccl", sync: bool = False):
+        import torch
+
+        self.torch = torch
+        self.ctx, self.tiles = ctx, tiles
+        self.width, self.height, self.rank, self.world, self.stripe = width, height, rank, world, stripe
+        self.spp_rank, self.dist, self.backend, self.sync = spp_rank, dist, backend, sync
+        self.npix = tile_pixels(tiles)
+        n = max(max_rank_pixels(width, height, world, stripe), self.npix)
+        self.out = torch.zeros((n, 4), dtype=torch.float32, device=f"cuda:{device}")
+        self.device = device
+        on_host = backend == "gloo"
+        self.gather = None
+        if dist is not None and rank == 0:
+            self.gather = [torch.empty((n, 4), dtype=torch.float32, device="cpu" if on_host else f"cuda:{device}")
+                           for _ in range(world)]
+        self.stream = torch.cuda.current_stream().cuda_stream
+        self.sample = 0
+        self.gather_ev = []
+        self.gather_s = []
+        self.sync_stats = []
+
+    def step(self):
+        torch = self.torch
+        if self.sync:
+            self.ctx.render_device(self.out.data_ptr(), self.tiles, self.sample, self.spp_rank)
+            self.sync_stats.append(self.ctx.launch_stats())  # each synchronous call is its own window
+        else:
+            self.ctx.render_device_async(self.out.data_ptr(), self.tiles, self.sample, self.spp_rank,
+                                         stream=self.stream)
+        self.sample += self.spp_rank
+        if self.dist is None:
+            return
+        if self.backend == "gloo":
+            import time
+
+            t0 = time.perf_counter()
+            host = self.out.cpu()  # ordered after the step's fold on torch's stream
+            self.dist.gather(host, gather_list=self.gather, dst=0)
+            self.gather_s.append(time.perf_counter() - t0)
+        else:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.dist.gather(self.out, gather_list=self.gather, dst=0)
+            e1.record()
+            self.gather_ev.append((e0, e1))
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def run(self, steps: int, warmup: int) -> dict:
+        """W untimed steps, then exactly `steps` steps between barrier + synchronize on both
+        sides; the elapsed time is the maximum over ranks.  Returns {elapsed_s, launch stats of
+        the timed steps, gather_ms_per_step}."""
+        import time
+
+        for _ in range(warmup):
+            self.step()
+        self.ctx.synchronize()
+        self.barrier()
+        self.gather_ev.clear()
+        self.gather_s.clear()
+        self.sync_stats.clear()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.ctx.synchronize()
+        self.barrier()
+        elapsed = time.perf_counter() - t0
+        if self.sync:
+            ls = {k: sum(s[k] for s in self.sync_stats)
+                  for k in ("render_ms", "trace_ms", "n_trace_launches", "n_timed_launches")}
+        else:
+            ls = self.ctx.launch_stats()
+        if self.dist is not None:
+            t = self.torch.tensor([elapsed], device="cpu" if self.backend == "gloo" else f"cuda:{self.device}")
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        res = {"elapsed_s": elapsed, "launch": ls}
+        if self.gather_ev:
+            res["gather_ms_per_step"] = sum(a.elapsed_time(b) for a, b in self.gather_ev) / len(self.gather_ev)
+        elif self.gather_s:
+            res["gather_ms_per_step"] = 1e3 * sum(self.gather_s) / len(self.gather_s)
+        return res
+
+    def frame(self):
+        """Rank 0: the last step's frame assembled from every rank's gathered buffer (H, W, 4) as
+        a host array (the single-rank frame for world 1); None elsewhere."""
+        if self.rank != 0:
+            return None
+        parts = self.gather if self.dist is not None else [self.out]
+        f = assemble(parts, self.width, self.height, self.world, self.stripe)
+        return f.cpu().numpy() if hasattr(f, "cpu") else f

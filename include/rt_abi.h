@@ -257,6 +257,15 @@ int rt_render_device_async(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
                            uint64_t sample_begin, uint32_t sample_count, float* out_rgba_device,
                            void* stream);
 
+/* The mean over samples [sample_begin, sample_begin + sample_count) alone, per pixel of `tiles`
+ * (RGBA f32, alpha 1, tiles concatenated): what one batch of the reference's GPU path returns
+ * (block_and_get_single_result, gpu_utils.rs:681-724, whose kernel folds the batch with a
+ * running mean from zero, trace.wgsl:277-318) before render_to_target_gpu folds batches into its
+ * running mean (draw_scene.rs:36).  Uses the same per-(pixel, absolute sample) streams as
+ * rt_render; the context's cumulative mean is not touched.  Synchronous. */
+int rt_render_range(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
+                    uint64_t sample_begin, uint32_t sample_count, float* out_rgba);
+
 /* Waits for every enqueued call of the ctx and closes its timing window. */
 int rt_synchronize(rt_ctx* ctx);
 
@@ -271,7 +280,8 @@ typedef struct rt_launch_stats {
     float render_ms;            /* same as rt_last_kernel_ms */
     float trace_ms;             /* sum over the trace kernel launches */
     uint32_t n_trace_launches;
-    uint32_t _pad0;
+    uint32_t n_timed_launches;  /* launches in trace_ms: the first 256 of a window (async calls
+                                   without rt_synchronize keep the event pool bounded) */
 } rt_launch_stats;
 int rt_last_launch_stats(const rt_ctx* ctx, rt_launch_stats* out);
 

@@ -931,6 +931,19 @@ extern "C" int oracle_render(const rt_scene_desc* scene, const rt_camera* cam,
                              const rt_render_info* info, const rt_tile* tiles, uint32_t n_tiles,
                              uint64_t sample_begin, uint32_t sample_count, int threads,
                              int accum_mode, float* out_rgba, oracle_counts* counts) {
+    return oracle_render_ex(scene, cam, info, tiles, n_tiles, sample_begin, sample_count, threads, accum_mode,
+                            0, out_rgba, counts);
+}
+
+// mean_base: the running mean's n for sample s is s - mean_base.  0 is render_to_target_cpu's
+// frame mean (draw_scene.rs:81-83); the first sample of a batch gives one batch's own mean, the
+// WGSL kernel's per-dispatch fold from zero (trace.wgsl:277-318) that block_and_get_single_result
+// returns (gpu_utils.rs:681-724).
+extern "C" int oracle_render_ex(const rt_scene_desc* scene, const rt_camera* cam,
+                                const rt_render_info* info, const rt_tile* tiles, uint32_t n_tiles,
+                                uint64_t sample_begin, uint32_t sample_count, int threads,
+                                int accum_mode, uint64_t mean_base, float* out_rgba, oracle_counts* counts) {
+    if (mean_base > sample_begin) return RT_ERR_INVALID_ARG;
     if (!scene || !cam || !info || !tiles || !out_rgba) return RT_ERR_INVALID_ARG;
     Scene s;
     if (!s.build(scene, info->kd_tree_depth)) return RT_ERR_INVALID_ARG;
@@ -963,14 +976,14 @@ extern "C" int oracle_render(const rt_scene_desc* scene, const rt_camera* cam,
                 uint32_t pix = (uint32_t)y * info->width + (uint32_t)x;
                 float* acc = out_rgba + 4 * p;
                 float pr = 0.f, pg = 0.f, pb = 0.f;
-                if (sample_begin > 0) { pr = acc[0]; pg = acc[1]; pb = acc[2]; }
+                if (sample_begin > mean_base) { pr = acc[0]; pg = acc[1]; pb = acc[2]; }
                 for (uint64_t sidx = sample_begin; sidx < sample_begin + sample_count; ++sidx) {
                     g_rng = rt_rng_init(info->seed, pix, sidx);
                     if (g_cnt) g_cnt->samples += 1;
                     Ray ray = rc.rand_ray(x, y, *cam);
                     V3 rgb = accum_mode == ORACLE_ACCUM_FORWARD ? radiance_forward(ray, s, ri)
                                                                 : radiance(ray, s, 0, ri).rgb;
-                    float sc = (float)sidx;  // draw_scene.rs:81-83
+                    float sc = (float)(sidx - mean_base);  // draw_scene.rs:81-83
                     pr = (rgb.x + (pr * sc)) / (sc + 1.0f);
                     pg = (rgb.y + (pg * sc)) / (sc + 1.0f);
                     pb = (rgb.z + (pb * sc)) / (sc + 1.0f);

@@ -43,6 +43,15 @@ int oracle_render(const rt_scene_desc* scene, const rt_camera* cam, const rt_ren
                   uint32_t sample_count, int threads, int accum_mode, float* out_rgba,
                   oracle_counts* counts);
 
+/* oracle_render with the running mean's n = sample - mean_base (mean_base <= sample_begin):
+ * mean_base = sample_begin gives the mean over this call's samples alone (one batch of the
+ * reference's GPU path, trace.wgsl:277-318); out_rgba is read as the accumulator only when
+ * sample_begin > mean_base. */
+int oracle_render_ex(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_info* info,
+                     const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                     uint32_t sample_count, int threads, int accum_mode, uint64_t mean_base,
+                     float* out_rgba, oracle_counts* counts);
+
 /* KdTree::build (kdtree.rs:26-56,107-137) as a pointer tree, then a canonical depth-first
  * pre-order dump: per node {is_leaf, axis, split bits | leaf count, first ref}; refs in
  * leaf order.  Returns number of nodes; call with NULL buffers to size. */

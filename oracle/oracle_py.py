@@ -32,6 +32,9 @@ def lib():
         _lib.oracle_render.restype = C.c_int
         _lib.oracle_render.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                        C.c_uint32, C.c_int, C.c_int, P_f, C.c_void_p]
+        _lib.oracle_render_ex.restype = C.c_int
+        _lib.oracle_render_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
+                                          C.c_uint32, C.c_int, C.c_int, C.c_uint64, P_f, C.c_void_p]
         _lib.oracle_kd_dump.restype = C.c_int
         _lib.oracle_kd_dump.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                         C.POINTER(C.c_uint32), P_f]
@@ -67,17 +70,19 @@ def _fp(a):
 
 
 def render(loaded, tiles, sample_begin=0, sample_count=1, threads=0, accum=ACCUM_RECURSIVE,
-           init=None, counts=False):
-    """oracle_render over `tiles` (list of (x0, y0, w, h)) -> (npix, 4) float32 [, counts]."""
+           init=None, counts=False, mean_base=0):
+    """oracle_render over `tiles` (list of (x0, y0, w, h)) -> (npix, 4) float32 [, counts].
+    `init`: the accumulator at sample_begin (used when sample_begin > mean_base); `mean_base`:
+    the running mean's n is sample - mean_base (sample_begin: the mean of this range alone)."""
     from rt_amd import abi  # the scene structs are the ABI's; the oracle does not call the product
 
     npix = int(sum(t[2] * t[3] for t in tiles))
     out = np.zeros((npix, 4), dtype=np.float32) if init is None else np.array(init, dtype=np.float32).copy()
     tarr = (abi.rt_tile * len(tiles))(*[abi.rt_tile(*map(int, t)) for t in tiles])
     cnt = Counts()
-    st = lib().oracle_render(C.addressof(loaded.desc), C.addressof(loaded.cam), C.addressof(loaded.info),
-                             C.addressof(tarr), len(tiles), int(sample_begin), int(sample_count), int(threads),
-                             int(accum), _fp(out), C.addressof(cnt) if counts else None)
+    st = lib().oracle_render_ex(C.addressof(loaded.desc), C.addressof(loaded.cam), C.addressof(loaded.info),
+                                C.addressof(tarr), len(tiles), int(sample_begin), int(sample_count), int(threads),
+                                int(accum), int(mean_base), _fp(out), C.addressof(cnt) if counts else None)
     if st != 0:
         raise RuntimeError(f"oracle_render status {st}")
     if counts:

@@ -30,3 +30,26 @@ def u8(img: np.ndarray) -> np.ndarray:
 
 def frac_u8_within(gpu, ref, lsb=1):
     return float((np.abs(u8(gpu) - u8(ref)).max(axis=1) <= lsb).mean())
+
+
+def worst_pixel(gpu: np.ndarray, ref: np.ndarray) -> dict:
+    """The pixel farthest outside (or nearest the edge of) the gate, for the test log."""
+    g, r = gpu[:, :3].astype(np.float64), ref[:, :3].astype(np.float64)
+    d = np.abs(g - r).max(axis=1) / np.maximum(1.0, np.abs(r).max(axis=1))
+    i = int(np.argmax(d)) if len(d) else 0
+    return {"index": i, "rel_err": float(d[i]) if len(d) else 0.0,
+            "gpu": gpu[i, :3].tolist() if len(d) else None, "ref": ref[i, :3].tolist() if len(d) else None}
+
+
+def assert_reference_order(gpu: np.ndarray, ref_recursive: np.ndarray, label: str = "") -> dict:
+    """The stated gate against the reference's own recursive accumulation order (radiance.rs:44,59;
+    SURVEY.md §8d): per-pixel L-inf <= REL_TOL * max(1, |ref|) on >= MIN_FRAC of the pixels, RGBA8
+    within 1 LSB on >= MIN_FRAC, mean-image relative error < 1e-3.  Prints the worst pixel."""
+    s = stats(gpu, ref_recursive)
+    s["frac_u8_1lsb"] = frac_u8_within(gpu, ref_recursive)
+    s["worst"] = worst_pixel(gpu, ref_recursive)
+    print(label, "vs recursive oracle", s)
+    assert s["frac_ok"] >= MIN_FRAC, s
+    assert s["frac_u8_1lsb"] >= MIN_FRAC, s
+    assert s["mean_rel_err"] < 1e-3, s
+    return s

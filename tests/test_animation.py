@@ -129,3 +129,25 @@ def test_rt_render_animation_frames(gpu_available, tmp_path):
     r = subprocess.run(args[:5] + [d2] + args[6:] + ["--frames", "1/2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert sorted(os.listdir(d2)) == ["2.png"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame", [0, 37, 133])
+def test_bounce_frame_against_oracle(gpu_available, oracle, frame):
+    """An animation frame (bounce_anim.yml: frame 0, frame 37 between keyframes, the last frame)
+    rendered on the device equals the forward oracle run on that frame's own scene description,
+    bit for bit, and is within the stated gate of the reference's recursive order
+    (renderer.rs:65-207 renders each frame as a still through the same path)."""
+    import parity
+    from rt_amd import render
+
+    fr = _native("bounce_anim").frame(frame)
+    fr.info.width, fr.info.height = 150, 300
+    tiles = [(0, 0, 150, 300)]
+    with render.Context(fr) as c:
+        g = c.render(tiles, 0, 4)
+    o = oracle.render(fr, tiles, 0, 4, accum=oracle.ACCUM_FORWARD)
+    assert np.array_equal(g, o), parity.stats(g, o)
+    assert g[:, :3].max() > 0
+    r = oracle.render(fr, tiles, 0, 4, accum=oracle.ACCUM_RECURSIVE)
+    parity.assert_reference_order(g, r, f"bounce_anim frame {frame}")

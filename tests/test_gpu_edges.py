@@ -103,3 +103,37 @@ def test_bad_tiles_are_rejected(gpu_available, walled, tiles):
         assert e.value.status == abi.RT_ERR_INVALID_ARG
         g = c.render([(0, 0, 8, 8)], 0, 1)
     assert g.shape == (64, 4) and (g[:, 3] == 1.0).all()
+
+
+def test_empty_leaves_with_stale_offsets(gpu_available, monkeypatch):
+    """A caller-supplied tree whose empty leaves keep large ref offsets (every third leaf of
+    spaceship_r1's tree emptied, its offset pointed at the last ref): the upload's ref-list
+    dedupe shrinks the ref array ~25x, so such an offset would lie far past the packed list.
+    Camera-ray packets (closest_packet, scalar loads ahead of the leaf's tests), the cooperative
+    search and the stackless kernels must read nothing for an empty leaf: all give the same image,
+    and it differs from the full tree's (the emptied leaves are visited)."""
+    from rt_amd import render
+    from conftest import load_scene
+
+    sc = load_scene("spaceship_r1", width=320, height=160)
+    tree = render.KdTree(sc.desc, int(sc.info.kd_tree_depth))
+    nodes = tree.nodes.copy()
+    leaves = np.flatnonzero((nodes[:, 1] & 3) == 3)
+    emptied = leaves[::3]
+    nodes[emptied, 0] = 0
+    nodes[emptied, 1] = ((tree.n_refs - 1) << 2) | 3
+    t = tree.as_struct(nodes=nodes)
+    imgs = {}
+    for cfg in (("1", "0"), ("0", "0"), ("1", "1")):
+        monkeypatch.setenv("RT_PACKET", cfg[0])
+        monkeypatch.setenv("RT_KD_RESTART", cfg[1])
+        with render.Context(sc, tree=t) as c:
+            imgs[cfg] = c.render(None, 0, 2)
+    ref = imgs[("1", "0")]
+    for cfg, g in imgs.items():
+        assert np.array_equal(g, ref), (cfg, parity.stats(g, ref))
+    monkeypatch.setenv("RT_PACKET", "1")
+    monkeypatch.setenv("RT_KD_RESTART", "0")
+    with render.Context(sc) as c:
+        full = c.render(None, 0, 2)
+    assert not np.array_equal(full, ref)

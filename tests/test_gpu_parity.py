@@ -432,45 +432,48 @@ def test_render_to_target_pipelined_equals_batches(gpu_available, scene_name, sp
 
 @pytest.mark.parametrize("scene_name,spp", [("walled", 9), ("triangles", 4), ("biplane", 3), ("spaceship_r1", 3),
                                             ("a380", 2)])
-def test_stackless_traversal_bit_invariant(gpu_available, monkeypatch, scene_name, spp):
+def test_stackless_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scene_name, spp):
     """Stackless kd-restart with push-down (RT_KD_RESTART=1: after a leaf, descend again from the
-    deepest node above the first push, entry = the leaf's exit) == the reference's stack
-    traversal (kdtree.rs:66-104), bit for bit, in the queue kernels."""
+    deepest node above the first push, entry = the leaf's exit) and the stackless kernel with the
+    leaves' triangles staged in LDS (RT_KD_RESTART=2) each render the forward oracle's image (the
+    reference's stack traversal, kdtree.rs:66-104), bit for bit, in the queue kernels."""
     from rt_amd import render
 
     sc = load_scene(scene_name)
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
-    imgs = {}
-    for rs in ("0", "1", "2"):  # 2: stackless with the leaves' triangles staged in LDS
+    o = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
+    for rs in ("0", "1", "2"):
         monkeypatch.setenv("RT_KD_RESTART", rs)
         with render.Context(sc) as c:
-            imgs[rs] = c.render(tiles, 0, spp)
-    assert np.array_equal(imgs["0"], imgs["1"]), parity.stats(imgs["1"], imgs["0"])
-    assert np.array_equal(imgs["0"], imgs["2"]), parity.stats(imgs["2"], imgs["0"])
+            g = c.render(tiles, 0, spp)
+        assert np.array_equal(g, o), (rs, parity.stats(g, o))
 
 
 @pytest.mark.parametrize("scene_name,spp", [("triangles", 4), ("biplane", 3), ("spaceship_r1", 3), ("a380", 2)])
-def test_packet_traversal_bit_invariant(gpu_available, monkeypatch, scene_name, spp):
+def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scene_name, spp):
     """Camera-ray packets (closest_packet: scalar-loaded nodes and leaf refs, per-lane
     near / far / push on the lane's own interval, deferred lanes, kd-restart from the packet's
-    restart node, hand-over to the cooperative search) and the 8 x 8 block queue order give the
-    cooperative search's images bit for bit (kdtree.rs:66-104), on two tiles and a full frame."""
+    restart node, hand-over to the cooperative search), the cooperative search alone
+    (RT_PACKET=0) and the row-order queue (RT_PIX_BLOCK=1) each render the forward oracle's image
+    (kdtree.rs:66-104), bit for bit, on two tiles and a full frame."""
     from rt_amd import render
 
     sc = load_scene(scene_name, width=320, height=160)
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
-    imgs = {}
+    o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
+    o_full = oracle.render(sc, [(0, 0, w, h)], 0, 2 * spp, accum=oracle.ACCUM_FORWARD)
     for cfg in (("1", "8"), ("0", "1"), ("1", "1"), ("0", "8")):
         monkeypatch.setenv("RT_PACKET", cfg[0])
         monkeypatch.setenv("RT_PIX_BLOCK", cfg[1])
         with render.Context(sc) as c:
-            imgs[cfg] = (c.render(tiles, 0, spp), c.render(None, spp, spp))
-    ref = imgs[("1", "8")]
-    for cfg, got in imgs.items():
-        for a, b in zip(got, ref):
-            assert np.array_equal(a, b), (cfg, parity.stats(a, b))
+            got = c.render(tiles, 0, spp)
+        assert np.array_equal(got, o_tiles), (cfg, parity.stats(got, o_tiles))
+        with render.Context(sc) as c:  # whole frame, two calls: [0, spp) then [spp, 2 spp)
+            c.render(None, 0, spp, want_output=False)
+            full = c.render(None, spp, spp)
+        assert np.array_equal(full, o_full), (cfg, parity.stats(full, o_full))
 
 
 def test_sphere_scene_with_lens_bit_exact(gpu_available, oracle):

@@ -25,23 +25,29 @@ def pick(frame, w, pts):
     return np.stack([frame[y * w + x] for (x, y) in pts])
 
 
-def test_walled_bench_launch_shape(gpu_available, oracle):
-    """walled.yml as bench.py's step runs it: one full-frame 1000-spp queue launch (720 M items),
-    here at sample_begin 19000 (the 20th step of the 20000-spp scheme)."""
+def test_walled_config4_whole_run(gpu_available, oracle):
+    """BASELINE config 4 as the bench runs it: walled.yml's whole 20000-spp run in its 1000-spp
+    full-frame queue launches (one launch per call, 720 M items each, the running mean carried on
+    the device from sample 0), then 256 scattered pixels against the oracle run over the same
+    [0, 20000): bit-exact against the forward oracle, and the stated gate against the reference's
+    own recursive order (radiance.rs:44,59)."""
     from rt_amd import render
 
     sc = load_scene("walled")
     w, h = int(sc.info.width), int(sc.info.height)
     pts = scattered(w, h, 256, seed=19)
     with render.Context(sc) as ctx:
-        frame = ctx.render(None, 19000, 1000)
-        n_launch = ctx.launch_stats()["n_trace_launches"]
-    assert n_launch == 1  # one queue launch, as in the bench
+        for s0 in range(0, 20000, 1000):
+            frame = ctx.render(None, s0, 1000, want_output=(s0 == 19000))
+            assert ctx.launch_stats()["n_trace_launches"] == 1  # one queue launch, as in the bench
     g = pick(frame, w, pts)
-    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 19000, 1000, accum=oracle.ACCUM_FORWARD)
+    tiles = [(x, y, 1, 1) for (x, y) in pts]
+    o = oracle.render(sc, tiles, 0, 20000, accum=oracle.ACCUM_FORWARD)
     s = parity.stats(g, o)
-    print("walled 1000 spp @19000", s)
+    print("walled [0, 20000) forward", s)
     assert np.array_equal(g, o), s
+    r = oracle.render(sc, tiles, 0, 20000, accum=oracle.ACCUM_RECURSIVE)
+    parity.assert_reference_order(g, r, "walled [0, 20000)")
 
 
 def test_spaceship_4096_config5(gpu_available, oracle):
@@ -81,10 +87,13 @@ def test_biplane_200spp_scheme_batches(gpu_available, oracle):
         for s0 in range(0, 200, 10):
             frame = ctx.render(None, s0, 10, want_output=(s0 == 190))
     g = pick(frame, w, pts)
-    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 0, 200, accum=oracle.ACCUM_FORWARD)
+    tiles = [(x, y, 1, 1) for (x, y) in pts]
+    o = oracle.render(sc, tiles, 0, 200, accum=oracle.ACCUM_FORWARD)
     s = parity.stats(g, o)
     print("biplane 200 spp", s)
     assert np.array_equal(g, o), s
+    r = oracle.render(sc, tiles, 0, 200, accum=oracle.ACCUM_RECURSIVE)
+    parity.assert_reference_order(g, r, "biplane 200 spp")
 
 
 def test_a380_batch1(gpu_available, oracle):
@@ -99,15 +108,21 @@ def test_a380_batch1(gpu_available, oracle):
         for s0 in range(10):
             frame = ctx.render(None, s0, 1, want_output=(s0 == 9))
     g = pick(frame, w, pts)
-    o = oracle.render(sc, [(x, y, 1, 1) for (x, y) in pts], 0, 10, accum=oracle.ACCUM_FORWARD)
+    tiles = [(x, y, 1, 1) for (x, y) in pts]
+    o = oracle.render(sc, tiles, 0, 10, accum=oracle.ACCUM_FORWARD)
     s = parity.stats(g, o)
     print("a380 batch 1", s)
     assert np.array_equal(g, o), s
+    r = oracle.render(sc, tiles, 0, 10, accum=oracle.ACCUM_RECURSIVE)
+    parity.assert_reference_order(g, r, "a380 batch 1")
 
 
 # Whole frames, every pixel: the oracle's cost per sample (CPU column) makes a full
 # 1200 x 600 frame at 1-10 spp a few seconds of host work, so each benchmark scene is compared on
 # its entire frame, in the scheme's own batch size where that is smaller than the sample count.
+# A range that starts past sample 0 continues a context that has rendered [0, s0) itself; the
+# oracle continues from that context's frame (its `init`), so both run the same samples from the
+# same state.
 WHOLE = [
     # scene, sample_begin, samples, batch, dir_light_samp
     ("triangles", 0, 10, 10, 0),       # BASELINE config 0: 10 spp, depth 5
@@ -116,23 +131,43 @@ WHOLE = [
     ("biplane", 190, 2, 1, 0),         # config 3's tail, one-sample batches (pipelined launches)
     ("spaceship_r1", 25, 1, 1, 0),
     ("a380", 3, 2, 1, 0),              # config 2's batch of 1
+    ("outside_spheres", 0, 2, 1, 0),   # schemes/outside_spheres.yml as a still (lens, cube map, kd depth 1)
     ("spaceship_r1@4096", 0, 1, 1, 0),  # config 5's 4096 x 4096 frame (16.8 M pixels)
 ]
 
 
+def _prefix_batch(name, s0):
+    """The batch the context renders [0, s0) in: the scheme's own gpu_render_batch where it
+    divides s0, else one call."""
+    b = {"walled": 1000, "biplane": 10, "spaceship_r1": 25, "a380": 1}.get(name, s0)
+    return b if s0 % b == 0 else s0
+
+
 @pytest.mark.parametrize("name,s0,spp,batch,dls", WHOLE, ids=[f"{w[0]}-dls{w[4]}" for w in WHOLE])
 def test_whole_frame_bit_exact(gpu_available, oracle, name, s0, spp, batch, dls):
+    """Every pixel bit-exact against the forward oracle, and within the stated gate against the
+    reference's recursive order (radiance.rs:44,59)."""
     from rt_amd import render
 
     scene, _, size = name.partition("@")
     sc = load_scene(scene, **({"width": int(size), "height": int(size)} if size else {}))
     sc.info.dir_light_samp = dls
     w, h = int(sc.info.width), int(sc.info.height)
+    init = None
     with render.Context(sc) as ctx:
+        if s0:  # [0, s0) on the device first: the range below continues an accumulated context
+            pb = _prefix_batch(scene, s0)
+            assert s0 % pb == 0
+            for b in range(0, s0, pb):
+                init = ctx.render(None, b, pb, want_output=(b + pb == s0))
         for b in range(s0, s0 + spp, batch):
             frame = ctx.render(None, b, batch, want_output=(b + batch == s0 + spp))
-    o = oracle.render(sc, [(0, 0, w, h)], s0, spp, accum=oracle.ACCUM_FORWARD)
+    full = [(0, 0, w, h)]
+    o = oracle.render(sc, full, s0, spp, accum=oracle.ACCUM_FORWARD, init=init)
     s = parity.stats(frame, o)
     print(f"{name} whole frame {w}x{h}, samples [{s0}, {s0 + spp}), dls {dls}", s)
     assert (frame[:, 3] == 1.0).all()
     assert np.array_equal(frame, o), s
+    del o
+    r = oracle.render(sc, full, s0, spp, accum=oracle.ACCUM_RECURSIVE, init=init)
+    parity.assert_reference_order(frame, r, f"{name} [{s0}, {s0 + spp})")

@@ -51,7 +51,8 @@ def test_scene_recursive_parity(scene, oracle):
     o = oracle.render(sc, crops, 0, spp, accum=oracle.ACCUM_RECURSIVE)
     s = parity.stats(g, o)
     print(name, "recursive", s)
-    assert s["frac_ok"] >= 0.995, s
+    assert s["frac_ok"] >= parity.MIN_FRAC, s
+    assert parity.frac_u8_within(g, o) >= parity.MIN_FRAC, s
     assert s["mean_rel_err"] < 1e-3
 
 

@@ -90,3 +90,25 @@ def test_assemble_single_rank_is_identity():
     buf = _pattern(w, h, shard.rank_tiles(w, h, 0, 1), w * h)
     frame = shard.assemble([buf], w, h, 1)
     assert np.array_equal(frame.reshape(-1, 4), buf)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_step_sample_accounting(world):
+    """bench.py's accounting (rt_amd.shard.step_samples): strong keeps the job at W*H*spp per step
+    whatever N, each rank spp per pixel of its 1/N of the frame; weak gives every rank the 1-GPU
+    step's work, W*H/N pixels at N*spp, so the job is N times the 1-GPU step."""
+    from rt_amd import shard
+
+    w, h, spp = 1200, 600, 1000
+    s_rank, s_job = shard.step_samples(w, h, spp, world, strong=True)
+    assert (s_rank, s_job) == (spp, w * h * spp)
+    w_rank, w_job = shard.step_samples(w, h, spp, world, strong=False)
+    assert (w_rank, w_job) == (spp * world, w * h * spp * world)
+    # every rank's share of one step, summed over ranks, is the job
+    stripe = shard.stripe_rows(h, world)
+    for spp_rank, job in ((s_rank, s_job), (w_rank, w_job)):
+        assert sum(shard.tile_pixels(shard.rank_tiles(w, h, r, world, stripe)) * spp_rank
+                   for r in range(world)) == job
+        # and with equal stripe counts each rank's share is job / N (balanced)
+        assert {shard.tile_pixels(shard.rank_tiles(w, h, r, world, stripe)) * spp_rank
+                for r in range(world)} == {job // world}
