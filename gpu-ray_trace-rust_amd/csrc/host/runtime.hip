@@ -6,12 +6,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -166,6 +168,67 @@ static DevMat make_mat(const rt_material& m, const float rgb[3]) {
     d.r0 = q * q;
     for (int i = 0; i < 3; ++i) d.rgb_atten[i] = d.rgb[i] / 0.4f;  // RR_THRES
     return d;
+}
+
+// Every texel channel of every texture as an 8-bit k with (float)k / 255.0f == the channel, bit
+// for bit (the value image::to_rgb32f makes of an 8-bit image), packed as RGBA8 words in pool
+// order; false at the first channel that is not (NaN, -0, values off the k / 255 grid).  Split
+// over a few threads: a380's 44 M texels take ~20 ms.
+static bool pack_texels_u8(const rt_scene_desc* scene, const std::vector<DevTex>& texs, uint64_t texel_count,
+                           std::vector<uint32_t>* out) {
+    uint32_t lut[256];
+    for (uint32_t k = 0; k < 256; ++k) {
+        const float f = (float)k / 255.0f;
+        std::memcpy(&lut[k], &f, 4);
+    }
+    out->assign(texel_count, 0u);
+    std::atomic<bool> ok{true};
+    auto work = [&](uint32_t t0, uint32_t t1, uint64_t p0, uint64_t p1) {
+        for (uint32_t i = t0; i < t1 && ok.load(std::memory_order_relaxed); ++i) {
+            const rt_texture& tx = scene->textures[i];
+            const uint64_t n = (uint64_t)tx.width * tx.height;
+            const uint64_t b = i == t0 ? p0 : 0, e = i + 1 == t1 && p1 ? p1 : n;
+            uint32_t* dst = out->data() + texs[i].off;
+            for (uint64_t q = b; q < e; ++q) {
+                uint32_t w = 0;
+                for (int ch = 0; ch < 3; ++ch) {
+                    const float v = tx.rgb[3 * q + (uint64_t)ch];
+                    const float s = v * 255.0f + 0.5f;  // k for v = k / 255 (NaN / negative fail below)
+                    if (!(s >= 0.0f && s < 256.0f)) { ok = false; return; }
+                    const uint32_t k = (uint32_t)s;
+                    uint32_t bits;
+                    std::memcpy(&bits, &v, 4);
+                    if (bits != lut[k]) { ok = false; return; }
+                    w |= k << (8 * ch);
+                }
+                dst[q] = w;
+            }
+        }
+    };
+    // split the pool into ~equal texel ranges: (texture, first texel) .. (texture, end texel)
+    const unsigned n_thr = std::max(1u, std::min(8u, (unsigned)(texel_count >> 20)));
+    std::vector<std::thread> pool;
+    uint64_t per = (texel_count + n_thr - 1) / n_thr;
+    uint32_t ti = 0;
+    uint64_t at = 0;  // texels before texture ti
+    for (unsigned k = 0; k < n_thr; ++k) {
+        const uint64_t g0 = k * per, g1 = std::min<uint64_t>(texel_count, g0 + per);
+        if (g0 >= g1) break;
+        while (ti < scene->n_textures && at + (uint64_t)scene->textures[ti].width * scene->textures[ti].height <= g0) {
+            at += (uint64_t)scene->textures[ti].width * scene->textures[ti].height;
+            ++ti;
+        }
+        // [g0, g1) in pool order: from texture ti at g0 - at to the texture holding g1 - 1
+        uint32_t tj = ti;
+        uint64_t at2 = at;
+        while (at2 + (uint64_t)scene->textures[tj].width * scene->textures[tj].height < g1) {
+            at2 += (uint64_t)scene->textures[tj].width * scene->textures[tj].height;
+            ++tj;
+        }
+        pool.emplace_back(work, ti, tj + 1, g0 - at, g1 - at2);
+    }
+    for (auto& th : pool) th.join();
+    return ok.load();
 }
 
 static void destroy_ctx(rt_ctx* c) {
@@ -407,16 +470,30 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
     if ((st = upload(c, ftri_n, &d.ftri_n))) return st;
     if ((st = upload(c, ftri_mat, &d.ftri_mat))) return st;
-    if (texel_count) {  // each texture straight from the caller's array into the pool (no host staging copy)
-        void* p = nullptr;
-        if (hipMalloc(&p, 3 * sizeof(float) * texel_count) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
-        c->allocs.push_back(p);
-        for (uint32_t i = 0; i < scene->n_textures; ++i) {
-            const rt_texture& tx = scene->textures[i];
-            HIPCHK(c, hipMemcpy(static_cast<float*>(p) + 3 * (size_t)texs[i].off, tx.rgb,
-                                3 * sizeof(float) * (size_t)tx.width * tx.height, hipMemcpyHostToDevice));
+    if (texel_count) {
+        // Textures decoded from 8-bit images hold k / 255 in every channel (image::to_rgb32f,
+        // model.rs:204): such a pool is stored as one RGBA8 word per texel (a third of the bytes:
+        // biplane 453 -> 151 MB, a380 525 -> 175 MB, under the 256 MB Infinity Cache) and decoded
+        // on the device bit for bit.  Any other value keeps the f32 pool, uploaded straight from
+        // the caller's arrays.
+        std::vector<uint32_t> t8;
+        if (!std::getenv("RT_TEXELS_F32") && pack_texels_u8(scene, texs, texel_count, &t8)) {
+            void* p = nullptr;
+            if (hipMalloc(&p, sizeof(uint32_t) * texel_count) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
+            c->allocs.push_back(p);
+            HIPCHK(c, hipMemcpy(p, t8.data(), sizeof(uint32_t) * texel_count, hipMemcpyHostToDevice));
+            d.texels8 = static_cast<const uint32_t*>(p);
+        } else {
+            void* p = nullptr;
+            if (hipMalloc(&p, 3 * sizeof(float) * texel_count) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
+            c->allocs.push_back(p);
+            for (uint32_t i = 0; i < scene->n_textures; ++i) {
+                const rt_texture& tx = scene->textures[i];
+                HIPCHK(c, hipMemcpy(static_cast<float*>(p) + 3 * (size_t)texs[i].off, tx.rgb,
+                                    3 * sizeof(float) * (size_t)tx.width * tx.height, hipMemcpyHostToDevice));
+            }
+            d.texels = static_cast<const float*>(p);
         }
-        d.texels = static_cast<const float*>(p);
     }
     if ((st = upload(c, texs, &d.tex))) return st;
     if ((st = upload(c, mtri, &d.mtri))) return st;

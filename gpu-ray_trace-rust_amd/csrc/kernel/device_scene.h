@@ -106,7 +106,11 @@ struct DevScene {
     const float2* uv_mr;
     // textures
     const DevTex* tex;
-    const float* texels;    // f32 RGB pool of every scene texture
+    // The texel pool of every scene texture: f32 RGB (texels), or — when every texel channel is
+    // some k / 255 in f32, as image::to_rgb32f makes them (uv_image.rs:9-23, model.rs:204) —
+    // one RGBA8 word per texel (texels8, A unused), decoded as k / 255 bit for bit.
+    const float* texels;
+    const uint32_t* texels8;
     // cube map (first unconditional renderable, distant_cube_map.rs); has_cube == 0: misses are black
     uint32_t has_cube;
     DevFace face[6];

@@ -108,6 +108,25 @@ __device__ __forceinline__ unsigned long long tm_now() {  // ordered stamp (cdna
 #define TM_ADD(i, v) do { } while (0)
 #endif
 
+// Diagnostic build only (-DRT_VMEM_COUNT=1): vector-memory load instructions of the general queue
+// kernel by class, counted once per wave execution of each load site (the first active lane adds
+// the site's instruction count to a global counter), printed by the last wave of each launch
+// (tools/vmem_classes.py).  Classes: 0 descent nodes, 1 pop nodes, 2 pass refs, 3 pass triangles,
+// 4 leading spheres, 5 winner re-test, 6 path-start pixel table, 7 mesh shading records,
+// 8 textures, 9 sphere / free-triangle shading, 10 packet leaf visits (scalar loads: no VMEM),
+// 11 cooperative passes, 12 cooperative rounds, 13 radiance stores (writes), 14 path starts.
+#ifndef RT_VMEM_COUNT
+#define RT_VMEM_COUNT 0
+#endif
+#if RT_VMEM_COUNT
+__device__ unsigned long long g_vc[24];
+__device__ unsigned int g_vc_waves;
+#define VC(i, n) do { if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
+                           atomicAdd(&g_vc[i], (unsigned long long)(n)); } while (0)
+#else
+#define VC(i, n) do { } while (0)
+#endif
+
 
 struct V3 {
     float x, y, z;
@@ -851,6 +870,7 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     // item w of a lane's leaf is sc.refs[w + delta]
     const uint32_t delta = off - (incl - cnt);
     for (uint32_t base = 0; base < total; base += 64) {
+        VC(11, 1);
         const uint32_t w = base + lane;
         const uint32_t owner = pass_owner(incl, total, base, w);
         const uint32_t idx = w + __shfl(delta, owner);
@@ -870,6 +890,8 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             } else {
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
+                VC(2, 1);
+                VC(3, 3);
                 ref = sc.refs[idx];
                 const float4* pd = prim_data(sc, ref);
                 a0 = pd[0];
@@ -923,6 +945,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             node = restart;
         } else {
             --sp;
+            VC(1, sp ? 2 : 1);
             const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
             float d;
             (void)split_t<FAST>(pn, ax, r, &d);
@@ -940,10 +963,13 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     while (__ballot(!done) != 0) {
         uint32_t off = 0, cnt = 0, list = ~0u;
         unsigned long long key0 = ~0ull;
+        VC(12, 1);
         if (!done) {
             uint2 nd = fetch_node(sc, node);
+            VC(0, 1);
             pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
+                VC(0, RT_PAIR_FETCH ? 2 : 1);
                 // RT_PAIR_FETCH: both children (adjacent, 16 B) are loaded before this node's
                 // decision, so the next level's fetch overlaps the decision's arithmetic
                 const uint32_t cpair = nd.y >> 2;
@@ -990,6 +1016,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 // lane's own tests; the wave's passes then hold triangles only.
                 const uint32_t lead = nd.x >> LEAF_LEAD_SHIFT;
                 for (uint32_t j = 0; j < lead; ++j) {
+                    VC(4, 2);
                     float l;
                     if (sphere_hit(prim_data(sc, sc.refs[off + j])[0], r, &l) && l >= HIT_MIN)
                         key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
@@ -1011,6 +1038,25 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
 #if RT_TIMING
         const unsigned long long tmc0 = TM_NOW();
 #endif
+#if RT_VMEM_COUNT
+        {   // leaf sharing in this round: groups of lanes at one leaf (equal offsets), their pairs
+            uint64_t pending = __ballot(cnt > 0);
+            while (pending) {
+                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
+                const uint32_t o = __builtin_amdgcn_readlane(off, ld), n = __builtin_amdgcn_readlane(cnt, ld);
+                const uint64_t same = __ballot(off == o && cnt > 0) & pending;
+                pending &= ~same;
+                const uint32_t g = (uint32_t)__popcll(same);
+                VC(15, n * g);
+                if (g >= 2) VC(16, n * g);
+                if (g >= 3) VC(17, n * g);
+                if (g >= 4) VC(18, n * g);
+                if (g >= 8) VC(19, n * g);
+                VC(20, n * ((g + 3u) / 4u));
+                VC(21, 1);
+            }
+        }
+#endif
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
 #if RT_TIMING
         TM_ADD(12, TM_NOW() - tmc0);
@@ -1027,6 +1073,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             // re-tested after every leaf).
             bool ret = key != ~0ull && __uint_as_float((uint32_t)(key >> 32)) <= exit_t + EPS;
             if (ret) {
+                VC(5, 4);
                 const uint32_t ref = sc.refs[(uint32_t)key];
                 const float4* pd = prim_data(sc, ref);
                 const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
@@ -1122,6 +1169,7 @@ __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax,
             nd = ps.nodes[node];
         }
         if (RT_PACKET_KEEP > 0 && __popcll(__ballot(act)) < RT_PACKET_KEEP) break;
+        VC(10, 1);
         TM_ADD(3, 1);
         TM_ADD(4, __popcll(__ballot(act)));
         TM_ADD(5, nd.x & LEAF_COUNT_MASK);
@@ -1294,6 +1342,13 @@ __device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float dn, V3 refl, float o
     return trns;
 }
 
+// k / 255.0f for an 8-bit k, bit for bit: the Markstein quotient with the exact reciprocal of
+// 255 (div_mk; equal to the IEEE division for all 256 k, tests/test_device_code.py), k = 0 exact.
+__device__ __forceinline__ float u8_over_255(uint32_t k) {
+    const float r = 0x1.010102p-8f;  // RN(1 / 255)
+    return div_mk((float)k, 255.0f, r);
+}
+
 // UVRgb32FImage::get_pixel (uv_image.rs:9-23): nearest texel, clamped, truncated; `as u32`
 // maps NaN to 0.
 __device__ __forceinline__ V3 get_pixel(const DevScene& sc, uint32_t off, uint32_t w, uint32_t h, float u,
@@ -1303,9 +1358,16 @@ __device__ __forceinline__ V3 get_pixel(const DevScene& sc, uint32_t off, uint32
     float fy = fminf(fmaxf(v * height, 0.0f), height - 1.0f);
     uint32_t x = __builtin_isnan(fx) ? 0u : (uint32_t)truncf(fx);
     uint32_t y = __builtin_isnan(fy) ? 0u : (uint32_t)truncf(fy);
-    return ld3(sc.texels + 3 * ((size_t)off + (size_t)y * w + x));
+    const size_t i = (size_t)off + (size_t)y * w + x;
+    VC(8, 1);
+    if (sc.texels8) {  // 4 B per texel instead of 12: each channel k / 255.0f, correctly rounded
+        const uint32_t t = sc.texels8[i];
+        return mk(u8_over_255(t & 0xffu), u8_over_255((t >> 8) & 0xffu), u8_over_255((t >> 16) & 0xffu));
+    }
+    return ld3(sc.texels + 3 * i);
 }
 __device__ __forceinline__ V3 tex_pixel(const DevScene& sc, int32_t t, float u, float v) {
+    VC(8, 1);
     const DevTex tx = sc.tex[t];
     return get_pixel(sc, tx.off, tx.w, tx.h, u, v);
 }
@@ -1421,6 +1483,7 @@ __device__ V3 dls_contrib(const DevScene& sc, const Path& p, uint32_t next) {
 __device__ __forceinline__ void tex_coord(const float2* uv, const DevMeshTri& t, float b1, float b2, float* u,
                                           float* v) {
     float b0 = 1.0f - b2 - b1;
+    VC(7, 3);
     float2 c0 = uv[t.v[0]], c1 = uv[t.v[1]], c2 = uv[t.v[2]];
     float su = 0.0f, sv = 0.0f;
     su = su + c0.x * b0;
@@ -1444,6 +1507,7 @@ template <bool COUNT>
 __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, uint32_t idx, Path& p,
                                           Ctr<COUNT>& c) {
     if (COUNT) c.mesh_hits++;
+    VC(7, 6);  // the 64-B triangle record and the 32-B primitive record
     const DevMeshTri t = sc.mtri[idx];
     const DevPrim pr = sc.prims[t.prim];
     const float b1 = h.bu, b2 = h.bv;
@@ -1454,6 +1518,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
         n = normalize(mul3(t.m, tex_pixel(sc, pr.normal_tex, u, v)));
     } else {
         V3 cum = mk(0.f, 0.f, 0.f);
+        VC(7, 3);
         cum = cum + xyz(sc.vnorm[t.v[0]]);
         cum = cum + xyz(sc.vnorm[t.v[1]]);
         cum = cum + xyz(sc.vnorm[t.v[2]]);
@@ -1517,6 +1582,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     if (GEN && kind == K_MESH_TRI) return mesh_segment<COUNT>(sc, h, idx - sc.pool_mesh, p, c);
     V3 n, pos;
     const DevMat* m;
+    if (GEN) VC(9, 6);
     if (!GEN || kind == K_SPHERE) {  // Sphere::hit_info (sphere.rs:64-80)
         float4 s = fetch_sphere<GEN>(sc, idx);
         V3 perfect = p.ray.o + p.ray.d * h.l;
@@ -1889,6 +1955,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                     int x, y;
                     uint64_t key;
                     V3 dir;
+                    if (GEN) { VC(6, 1); VC(14, 1); }
                     if (a.pix_q) {  // item j * n_pix + q: the q-th pixel in queue order
                         const uint4 e = a.pix_q[o];
                         x = (int)(e.x & 0xffffu);
@@ -1921,6 +1988,14 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         tq_regen += TM_NOW() - tq0;
 #endif
         if (__ballot(have) == 0) {
+#if RT_VMEM_COUNT
+            if (GEN && __lane_id() == 0 && atomicAdd(&g_vc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+                __threadfence();
+                for (int i = 0; i < 24; ++i) printf("RT_VC %d %llu\n", i, g_vc[i]);
+                for (int i = 0; i < 24; ++i) g_vc[i] = 0;
+                g_vc_waves = 0;
+            }
+#endif
 #if RT_TIMING
             TM_ADD(2, TM_NOW() - tm_start);
             if (!GEN) {
@@ -1968,6 +2043,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
 #endif
         if (fin) {
+            if (GEN) VC(13, 1);
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;
             r[1] = p.L.y;

@@ -21,6 +21,12 @@
  * every float in [0, 2*pi] and in [0, 1] for powf(x, 5): tools/check_libm.c) and on the GPU by
  * tools/check_libm_gpu.hip.  Plain C: compiled unchanged by gcc and by hipcc for gfx950 (device
  * functions there).
+ *
+ * Licence of the restated algorithms and tables: the sinf / cosf / powf code and its data tables
+ * come from ARM's optimized-routines, "Copyright (c) 2017-2018, Arm Limited.", distributed with
+ * glibc under the GNU Lesser General Public License v2.1 or later (glibc 2.35,
+ * sysdeps/ieee754/flt-32) and by Arm under the MIT License (optimized-routines, math/).  The
+ * tables below are those published values; the notice above is kept with them.
  */
 #ifndef RT_LIBM_H
 #define RT_LIBM_H

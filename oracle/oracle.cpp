@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -73,7 +74,14 @@ static inline M3 mul(const M3& a, const M3& b) {
 // The reference's thread_rng() is replaced by the rt_rng.h stream of the current
 // (pixel, sample); every `crate::RNG.with_borrow_mut(|r| r.gen())` is one rng_f32().
 static thread_local rt_rng_state g_rng;
-static inline float rng_f32() { return rt_rng_next_f32(&g_rng); }
+// Shading-mix instrumentation (counted renders only, tools/min_insts.py): per continued ray by
+// branch, the draws, and the Russian-roulette draws.
+enum { MIX_SPEC, MIX_DIFF, MIX_DIFFSPEC_DIFF, MIX_DIFFSPEC_SPEC, MIX_DIELECTRIC, MIX_RR, MIX_DRAWS, MIX_MESH, MIX_N };
+static thread_local uint64_t* g_mix = nullptr;
+#define MIX(i) do { if (g_mix) g_mix[i]++; } while (0)
+static std::mutex g_mix_mu;
+static uint64_t g_mix_total[MIX_N];
+static inline float rng_f32() { MIX(MIX_DRAWS); return rt_rng_next_f32(&g_rng); }
 
 // ------------------------------------------------------------------ instrumentation
 static thread_local oracle_counts* g_cnt = nullptr;
@@ -224,12 +232,14 @@ static bool should_dls(const rt_material& m, const Seeding& s) {
 static Ray gen_new_ray(const rt_material& m, const Ray& ray, V3 n, V3 o, const Seeding& s,
                        float* p) {
     switch (m.divert) {
-        case RT_DIVERT_SPEC: *p = 1.0f; return spec(ray, n, o);
-        case RT_DIVERT_DIFF: *p = 1.0f; return diff(ray, n, o);
+        case RT_DIVERT_SPEC: MIX(MIX_SPEC); *p = 1.0f; return spec(ray, n, o);
+        case RT_DIVERT_DIFF: MIX(MIX_DIFF); *p = 1.0f; return diff(ray, n, o);
         case RT_DIVERT_DIFFSPEC:
+            MIX(s.diff ? MIX_DIFFSPEC_DIFF : MIX_DIFFSPEC_SPEC);
             *p = 1.0f;
             return s.diff ? diff(ray, n, o) : spec(ray, n, o);
         default:
+            MIX(MIX_DIELECTRIC);
             return refract(ray, n, o, m.n_out, m.n_in, p, [] { return rng_f32(); });
     }
 }
@@ -590,6 +600,7 @@ struct MeshTri final : Element {
     }
     bool continue_ray(const Ray& ray, const HitInfo& hi, V3* rgb, Ray* out) const override {
         // divert_new_ray (mesh/triangle.rs:209-225) then get_rgb (generic.rs:64)
+        MIX(MIX_MESH);
         Ray r = hi.seed.diff ? diff(ray, hi.norm, hi.pos) : spec(ray, hi.norm, hi.pos);
         float u = rng_f32();
         float v = rng_f32();
@@ -771,6 +782,7 @@ struct RadInfo { bool debug_single_ray, dir_light_samp; int assured_depth; int a
 // russian_roulette_filter (radiance.rs:74-86); max_thres is ignored by the reference.
 static bool russian_roulette(int depth, int assured, float* atten) {
     if (depth > assured) {
+        MIX(MIX_RR);
         float rr = rng_f32();
         static const float THRES = 0.4f;
         if (rr < THRES) { *atten = THRES; return true; }
@@ -962,6 +974,17 @@ extern "C" int oracle_render_ex(const rt_scene_desc* scene, const rt_camera* cam
     std::memset(per.data(), 0, sizeof(oracle_counts) * per.size());
     auto worker = [&](int tid) {
         g_cnt = counts ? &per[tid] : nullptr;
+        uint64_t mix[MIX_N] = {0};
+        g_mix = counts ? mix : nullptr;
+        struct Flush {
+            uint64_t* m;
+            ~Flush() {
+                if (!g_mix) return;
+                std::lock_guard<std::mutex> lk(g_mix_mu);
+                for (int i = 0; i < MIX_N; ++i) g_mix_total[i] += m[i];
+                g_mix = nullptr;
+            }
+        } flush{mix};
         const uint64_t CH = 16;  // rayon-like dynamic chunks of pixels
         for (;;) {
             uint64_t b = next.fetch_add(CH);
@@ -1110,4 +1133,15 @@ extern "C" void oracle_refract(const float d[3], const float n[3], float n_out, 
     Ray r = refract(Ray{mk(d), mk(0.f, 0.f, 0.f)}, mk(n), mk(0.f, 0.f, 0.f), n_out, n_in, p,
                     [u] { return u; });
     d_out[0] = r.d.x; d_out[1] = r.d.y; d_out[2] = r.d.z;
+}
+
+// Shading mix of the counted renders since the last reset (continued rays by material branch:
+// spec, diff, diffspec->diff, diffspec->spec, dielectric; Russian-roulette draws; all draws;
+// mesh continues), for tools/min_insts.py.
+extern "C" void oracle_mix_counts(uint64_t out[8], int reset) {
+    std::lock_guard<std::mutex> lk(g_mix_mu);
+    for (int i = 0; i < MIX_N; ++i) {
+        out[i] = g_mix_total[i];
+        if (reset) g_mix_total[i] = 0;
+    }
 }

@@ -52,6 +52,11 @@ int oracle_render_ex(const rt_scene_desc* scene, const rt_camera* cam, const rt_
                      uint32_t sample_count, int threads, int accum_mode, uint64_t mean_base,
                      float* out_rgba, oracle_counts* counts);
 
+/* Shading mix of the counted renders (counts != NULL) since the last reset: continued rays by
+ * material branch {spec, diff, diffspec->diff, diffspec->spec, dielectric}, Russian-roulette
+ * draws, all draws, mesh continues. */
+void oracle_mix_counts(uint64_t out[8], int reset);
+
 /* KdTree::build (kdtree.rs:26-56,107-137) as a pointer tree, then a canonical depth-first
  * pre-order dump: per node {is_leaf, axis, split bits | leaf count, first ref}; refs in
  * leaf order.  Returns number of nodes; call with NULL buffers to size. */

@@ -35,6 +35,8 @@ def lib():
         _lib.oracle_render_ex.restype = C.c_int
         _lib.oracle_render_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                           C.c_uint32, C.c_int, C.c_int, C.c_uint64, P_f, C.c_void_p]
+        _lib.oracle_mix_counts.restype = None
+        _lib.oracle_mix_counts.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         _lib.oracle_kd_dump.restype = C.c_int
         _lib.oracle_kd_dump.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                         C.POINTER(C.c_uint32), P_f]
@@ -109,3 +111,13 @@ def mesh_normal_transforms(desc, n_tris):
     if k < 0:
         raise RuntimeError("oracle_mesh_normal_transforms failed")
     return out[:k]
+
+
+MIX_FIELDS = ("spec", "diff", "diffspec_diff", "diffspec_spec", "dielectric", "rr_draws", "draws", "mesh")
+
+
+def mix_counts(reset=True):
+    """Shading mix of the counted renders (render(..., counts=True)) since the last reset."""
+    out = (C.c_uint64 * 8)()
+    lib().oracle_mix_counts(out, int(reset))
+    return dict(zip(MIX_FIELDS, (int(v) for v in out)))

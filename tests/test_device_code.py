@@ -57,3 +57,36 @@ def test_every_kernel_has_a_body():
         if "kernel" in name:
             assert size > 256, f"{name}: {size} B of code (an empty kernel is 4)"
     assert min(queue.values()) > 8192, queue
+
+
+def test_u8_over_255_markstein_is_exact(tmp_path):
+    """trace.hip u8_over_255: the texel decode of the 8-bit pool, q0 = k * r, q = fma(fma(-q0,
+    255, k), r, q0) with r = RN(1 / 255), equals the IEEE k / 255.0f (image::to_rgb32f's value)
+    for every k in 0..255, so the 8-bit pool renders the f32 pool's bits.  C fmaf is correctly
+    rounded (glibc), as v_fma_f32 is."""
+    import subprocess
+
+    src = tmp_path / "u8.c"
+    src.write_text(r'''
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+int main(void) {
+    const float r = 0x1.010102p-8f;
+    if (r != 1.0f / 255.0f) return 2;
+    int bad = 0;
+    for (unsigned k = 0; k < 256; ++k) {
+        float a = (float)k, q0 = a * r;
+        float q = fmaf(fmaf(-q0, 255.0f, a), r, q0);
+        if (k == 0) q = a;  /* div_mk's zero case */
+        float want = (float)k / 255.0f;
+        if (memcmp(&q, &want, 4)) bad++;
+    }
+    printf("%d\n", bad);
+    return bad != 0;
+}
+''')
+    exe = tmp_path / "u8"
+    subprocess.run(["gcc", "-O0", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout

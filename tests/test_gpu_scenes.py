@@ -69,3 +69,38 @@ def test_debug_single_ray_scene(scene, oracle):
     o = oracle.render(sc, crops, 0, 2)
     s = parity.stats(g, o)
     assert s["frac_exact"] == 1.0, s  # the lens's sin/cos are glibc's (rt_libm.h)
+
+
+@pytest.mark.parametrize("name", ["triangles", "biplane", "spaceship_r1"])
+def test_texel_pool_u8_equals_f32(gpu_available, monkeypatch, name):
+    """The 8-bit texel pool (every channel some k / 255: one RGBA8 word per texel, decoded on the
+    device) renders the f32 pool's image bit for bit (RT_TEXELS_F32=1 forces the f32 pool)."""
+    from rt_amd import render
+
+    sc = load_scene(name, width=320, height=160)
+    with render.Context(sc) as c:
+        g8 = c.render(None, 0, 3)
+    monkeypatch.setenv("RT_TEXELS_F32", "1")
+    with render.Context(sc) as c:
+        g32 = c.render(None, 0, 3)
+    assert np.array_equal(g8, g32), parity.stats(g8, g32)
+
+
+def test_texture_off_the_u8_grid_keeps_f32(gpu_available, oracle):
+    """A texel that is not k / 255 (here 0.123) cannot go to the 8-bit pool: the context keeps the
+    f32 pool and still renders the oracle's image."""
+    import ctypes as C
+
+    from rt_amd import render
+
+    sc = load_scene("triangles", width=320, height=160)
+    for i in range(sc.desc.n_textures):
+        t = sc.desc.textures[i]
+        px = C.cast(t.rgb, C.POINTER(C.c_float))
+        for k in range(0, 3 * t.width * t.height, 997):
+            px[k] = 0.123
+    tiles = [(0, 0, 320, 160)]
+    with render.Context(sc) as c:
+        g = c.render(tiles, 0, 2)
+    o = oracle.render(sc, tiles, 0, 2, accum=oracle.ACCUM_FORWARD)
+    assert np.array_equal(g, o), parity.stats(g, o)

@@ -76,6 +76,8 @@ def main(tag):
                          f"{2 * d['FETCH_SIZE'] / 1024:.2f} MB read from HBM per launch.")
         if "SQ_INSTS_VALU" in d:
             cnt["valu_insts_per_launch"] = d["SQ_INSTS_VALU"]
+        if "SQ_INSTS_VMEM_RD" in d:
+            cnt["vmem_rd_per_launch"] = d["SQ_INSTS_VMEM_RD"]
         if "SQ_THREAD_CYCLES_VALU" in d and d.get("SQ_ACTIVE_INST_VALU"):
             cnt["valu_lane_util"] = round(d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_ACTIVE_INST_VALU"]), 4)
             lines.append(f"\nLast dispatch: VALU lane utilisation = THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU) = "

@@ -10,7 +10,7 @@
 # Usage: tools/run_profiles.sh <tag> [bench args...]; then python tools/prof_summary.py <tag>
 set -o pipefail
 TAG=${1:-r2}; shift
-ARGS=${@:---steps 2 --warmup 1}
+ARGS=${@:---steps 2 --warmup 1 --no-configs}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT

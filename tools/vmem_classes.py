@@ -1,0 +1,74 @@
+"""Vector-memory load instructions of the general queue kernel by class, per sample (the
+RT_VMEM_COUNT diagnostic build: tools/build_variants.sh vmemcount="-DRT_VMEM_COUNT=1").
+Renders one full-frame launch of each scene in a child process (the kernel's printf goes to the
+child's stdout) and prints one JSON line per scene: wave-level load instructions per sample by
+class, next to SQ_INSTS_VMEM_RD per sample from the committed counters of the product build.
+Usage (on the GPU box): python tools/vmem_classes.py [scene:spp ...] > profiles/<tag>_vmem_classes.jsonl"""
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade",
+         "pk_leaves", "passes", "rounds", "rad_stores", "starts"]
+LOADS = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade"]
+
+CHILD = r"""
+import os, sys
+sys.path.insert(0, os.path.join(%(root)r, "gpu-ray_trace-rust_amd"))
+import torch  # noqa: F401
+from rt_amd import abi, render, scheme
+lib = abi.load_library(os.path.join(%(root)r, "gpu-ray_trace-rust_amd", "lib", "variants", "librt_vmemcount.so"))
+sch = scheme.load_json(os.path.join(%(root)r, "tests", "golden", "scenes", %(scene)r + ".json"))
+loaded = scheme.load(sch, assets_root=os.path.join(%(root)r, "assets_pack"), lib=lib)
+with render.Context(loaded, lib=lib) as c:
+    c.render(None, 0, %(spp)d, want_output=False)
+    c.render(None, %(spp)d, %(spp)d, want_output=False)
+print("PIXELS", int(loaded.info.width) * int(loaded.info.height), flush=True)
+"""
+
+
+def main(specs):
+    for spec in specs:
+        scene, _, spp = spec.partition(":")
+        spp = int(spp or 10)
+        code = CHILD % {"root": ROOT, "scene": scene, "spp": spp}
+        # serialized launches: the counters are per launch (overlapped launches would mix them)
+        env = dict(os.environ, RT_PIPELINE="0")
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, env=env)
+        # one "RT_VC <class> <count>" line per class and launch; the second launch's (the last 24)
+        vc = [l.split() for l in r.stdout.splitlines() if l.startswith("RT_VC ")]
+        pix = int(re.search(r"PIXELS (\d+)", r.stdout).group(1))
+        if len(vc) < 48:
+            print(json.dumps({"scene": scene, "error": r.stderr[-2000:]}))
+            continue
+        last = {int(c): int(v) for _, c, v in vc[-24:]}
+        d = {k: last[i] for i, k in enumerate(NAMES)}
+        gn = ["pairs", "pairs_g2", "pairs_g3", "pairs_g4", "pairs_g8", "quads", "groups"]
+        g = {k: last[15 + i] for i, k in enumerate(gn)}
+        samples = pix * spp  # the second launch (the first warms up; each launch prints its own)
+        per = {k: round(d[k] / samples, 3) for k in NAMES}
+        out = {"scene": scene, "spp_per_launch": spp, "samples": samples, "per_sample": per,
+               "vmem_loads_per_sample": round(sum(d[k] for k in LOADS) / samples, 2)}
+        if g.get("pairs"):
+            # cooperative pairs by the number of the wave's lanes at the same leaf in that round
+            out["leaf_sharing"] = {"pairs_per_sample": round(g["pairs"] / samples, 2),
+                                   "frac_pairs_in_groups_ge2": round(g["pairs_g2"] / g["pairs"], 4),
+                                   "frac_ge3": round(g["pairs_g3"] / g["pairs"], 4),
+                                   "frac_ge4": round(g["pairs_g4"] / g["pairs"], 4),
+                                   "frac_ge8": round(g["pairs_g8"] / g["pairs"], 4),
+                                   "quad_slots_per_pair": round(4 * g["quads"] / g["pairs"], 4),
+                                   "pairs_per_group": round(g["pairs"] / g["groups"], 2)}
+        for p in sorted(os.listdir(os.path.join(ROOT, "profiles"))):
+            if p.endswith("_counters.json"):
+                c = json.load(open(os.path.join(ROOT, "profiles", p)))
+                if c.get("scene") == scene and c.get("vmem_rd_per_launch"):
+                    out["product_sq_insts_vmem_rd_per_sample"] = (
+                        round(c["vmem_rd_per_launch"] / c["samples_per_launch"], 2), p)
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["biplane:10", "spaceship_r1:10", "a380:4"])
