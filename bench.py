@@ -207,7 +207,7 @@ def cgroup_cpus():
 
 def cpu_baseline(loaded, spp, threads=None):
     """The oracle (C++ restatement of render_to_target_cpu, recursive radiance) over the full
-    frame at `spp` samples per pixel, one thread per CPU the process may run on
+    frame at `spp` samples per pixel, one thread per CPU the process may use
     (the reference's rayon par_iter_mut uses all of them, draw_scene.rs:73).  The KD build and
     scene setup are timed apart (an oracle call with 0 samples), as SURVEY.md §8d asks.  `cores`
     is the CPU time actually available: the thread count capped by the cgroup's CPU quota."""
@@ -215,8 +215,10 @@ def cpu_baseline(loaded, spp, threads=None):
     import oracle_py  # test infrastructure: the CPU baseline leg only
 
     affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = threads or affinity
     quota = cgroup_cpus()
+    # one thread per CPU of time the process may use: the CPUs it may run on, capped by the cgroup
+    # quota (256 threads under a 16-CPU quota only contend for the same 16 CPUs' time)
+    threads = threads or max(1, min(affinity, int(quota + 0.5) if quota else affinity))
     w, h = int(loaded.info.width), int(loaded.info.height)
     full = [(0, 0, w, h)]
 

@@ -1,6 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-for s in biplane spaceship_r1; do
-timeout -k 10 200 python -u tools/variant_bench.py --scene $s --spp 40 --rounds 3 noquad main qnone q7w noquad7w > gpurun_out/ab_q2_$s.log 2>&1 || exit 3
-grep -E "identical|variant" gpurun_out/ab_q2_$s.log
-done
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/b_default.json 2>gpurun_out/b_default.err || { tail -5 gpurun_out/b_default.err; exit 1; }
+python -c "
+import json; d=json.load(open('gpurun_out/b_default.json'))
+print(d['value'], d['roofline']['bound'], d['roofline']['frac'], d['roofline'].get('valu',{}).get('min_insts_frac'))
+for k,v in d['configs'].items(): print(k, v['value'], v['roofline']['bound'], v['roofline']['frac'], v['cpu_baseline']['value'], v['speedup_vs_cpu'])
+"
