@@ -10,11 +10,15 @@
 // kdtree.rs:119-127); a node is a leaf when depth > max_depth or it holds <= 1 element.
 #include "host_internal.h"
 
+#include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <new>
+#include <thread>
 #include <vector>
 
 namespace rth {
@@ -142,6 +146,119 @@ struct KdTreeOwned {
     std::vector<uint32_t> uncond;
 };
 
+// One node of a subtree built on its own (local indices): a branch {split, axis, low child}, or
+// a leaf {its refs in the subtree's ref list}; `ext` >= 0 marks a frontier node of the top part
+// whose subtree was built separately.
+struct SubNode {
+    uint32_t a = 0;          // split bits (branch) or ref count (leaf)
+    uint32_t axis = 0;       // RT_KD_LEAF for a leaf
+    uint32_t low = 0;        // low child (local), branch only
+    uint32_t ref_off = 0;    // leaf only
+    int32_t ext = -1;        // frontier: index of the separately built subtree
+};
+struct SubTree {
+    std::vector<SubNode> nodes;
+    std::vector<uint32_t> refs;
+    uint32_t max_leaf_depth = 0;
+};
+struct Frontier {
+    uint32_t depth;
+    std::vector<uint32_t> elems;
+};
+
+// node_from_elems (kdtree.rs:107-137), breadth first, from (elems, depth0).  Items reaching
+// depth `stop` (when frontier != nullptr) are not expanded: they become frontier nodes, built
+// later as subtrees of their own.  The node order within the subtree is the breadth-first order
+// of the whole build restricted to it, so merging (merge_bfs) reproduces the sequential numbering.
+static void build_subtree(const std::vector<Renderable>& rs, const std::vector<float>& cen, std::vector<uint32_t> elems,
+                          uint32_t depth0, uint32_t max_depth, uint32_t stop, SubTree* out,
+                          std::vector<Frontier>* frontier) {
+    // Level by level: a level's element lists concatenated in one array (no per-node vectors),
+    // its items in breadth-first order; the children of level L are level L + 1, in order.
+    struct Item { uint32_t node; uint32_t begin, end; };
+    std::vector<uint32_t> cur = std::move(elems), nxt;
+    std::vector<Item> items{Item{0, 0, (uint32_t)cur.size()}}, nitems;
+    out->nodes.emplace_back();
+    for (uint32_t depth = depth0; !items.empty(); ++depth) {
+        nxt.clear();
+        nitems.clear();
+        const uint32_t axis = depth % 3;
+        for (const Item& it : items) {
+            SubNode& nd = out->nodes[it.node];
+            const uint32_t n = it.end - it.begin;
+            if (frontier && depth == stop) {
+                nd.ext = (int32_t)frontier->size();
+                frontier->push_back(Frontier{depth, std::vector<uint32_t>(cur.begin() + it.begin, cur.begin() + it.end)});
+                continue;
+            }
+            if (depth > max_depth || n <= 1) {
+                nd.a = n;
+                nd.axis = RT_KD_LEAF;
+                nd.ref_off = (uint32_t)out->refs.size();
+                out->refs.insert(out->refs.end(), cur.begin() + it.begin, cur.begin() + it.end);
+                if (depth > out->max_leaf_depth) out->max_leaf_depth = depth;
+                continue;
+            }
+            float sum = 0.0f;  // centroid component on `axis`, folded in element order (kdtree.rs:113)
+            for (uint32_t k = it.begin; k < it.end; ++k) sum = sum + cen[3 * (size_t)cur[k] + axis];
+            const float split = sum / (float)n;
+            const uint32_t child = (uint32_t)out->nodes.size();
+            std::memcpy(&nd.a, &split, 4);
+            nd.axis = axis;
+            nd.low = child;
+            const uint32_t lb = (uint32_t)nxt.size();
+            for (uint32_t k = it.begin; k < it.end; ++k)
+                if (rs[cur[k]].lo[axis] <= split) nxt.push_back(cur[k]);
+            const uint32_t hb = (uint32_t)nxt.size();
+            for (uint32_t k = it.begin; k < it.end; ++k)
+                if (rs[cur[k]].hi[axis] >= split) nxt.push_back(cur[k]);
+            nitems.push_back(Item{child, lb, hb});
+            nitems.push_back(Item{child + 1, hb, (uint32_t)nxt.size()});
+            out->nodes.emplace_back();
+            out->nodes.emplace_back();
+        }
+        cur.swap(nxt);
+        items.swap(nitems);
+    }
+}
+
+// The whole tree in the sequential build's breadth-first numbering: a node's index is its
+// position in the breadth-first order, children appended as their parent is processed, and leaf
+// refs appended as each leaf is processed.
+static int merge_bfs(const SubTree& top, const std::vector<SubTree>& subs, KdTreeOwned* kt) {
+    struct Ref { uint32_t tree; uint32_t node; };  // tree UINT32_MAX: the top part
+    auto resolve = [&](Ref r) {
+        if (r.tree == UINT32_MAX && top.nodes[r.node].ext >= 0) return Ref{(uint32_t)top.nodes[r.node].ext, 0u};
+        return r;
+    };
+    auto node_of = [&](Ref r) -> const SubNode& { return r.tree == UINT32_MAX ? top.nodes[r.node] : subs[r.tree].nodes[r.node]; };
+    auto refs_of = [&](Ref r) -> const std::vector<uint32_t>& { return r.tree == UINT32_MAX ? top.refs : subs[r.tree].refs; };
+    size_t total = top.nodes.size();
+    for (const SubTree& t : subs) total += t.nodes.size() - 1;
+    if (total >= (1u << 30)) return RT_ERR_OOM;
+    kt->nodes.assign(total, rt_kd_node{0, 0});
+    std::vector<Ref> order;  // breadth-first: order[i] is global node i
+    order.reserve(total);
+    order.push_back(resolve(Ref{UINT32_MAX, 0}));
+    for (size_t i = 0; i < order.size(); ++i) {
+        const SubNode& nd = node_of(order[i]);
+        if (nd.axis == RT_KD_LEAF) {
+            const std::vector<uint32_t>& rf = refs_of(order[i]);
+            if (kt->refs.size() + nd.a >= (1u << 30)) return RT_ERR_OOM;
+            kt->nodes[i].a = nd.a;
+            kt->nodes[i].b = ((uint32_t)kt->refs.size() << 2) | RT_KD_LEAF;
+            kt->refs.insert(kt->refs.end(), rf.begin() + nd.ref_off, rf.begin() + nd.ref_off + nd.a);
+            continue;
+        }
+        const uint32_t child = (uint32_t)order.size();
+        kt->nodes[i].a = nd.a;
+        kt->nodes[i].b = (child << 2) | nd.axis;
+        order.push_back(resolve(Ref{order[i].tree, nd.low}));
+        order.push_back(resolve(Ref{order[i].tree, nd.low + 1}));
+    }
+    return order.size() == total ? RT_OK : RT_ERR_INVALID_ARG;
+}
+
 extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd_tree** out) {
     if (!scene || !out) return RT_ERR_INVALID_ARG;
     *out = nullptr;
@@ -170,40 +287,34 @@ extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd
             kt->pub.bounds[2 * a] = lo;
             kt->pub.bounds[2 * a + 1] = hi;
         }
-        struct Item { uint32_t node; uint32_t depth; std::vector<uint32_t> elems; };
-        std::deque<Item> q;
-        kt->nodes.push_back(rt_kd_node{0, 0});
-        q.push_back(Item{0, 0, std::move(root)});
-        while (!q.empty()) {
-            Item it = std::move(q.front());
-            q.pop_front();
-            const uint32_t axis = it.depth % 3;
-            if (it.depth > max_depth || it.elems.size() <= 1) {
-                if (kt->refs.size() + it.elems.size() >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
-                kt->nodes[it.node].a = (uint32_t)it.elems.size();
-                kt->nodes[it.node].b = ((uint32_t)kt->refs.size() << 2) | RT_KD_LEAF;
-                kt->refs.insert(kt->refs.end(), it.elems.begin(), it.elems.end());
-                if (it.depth > max_leaf_depth) max_leaf_depth = it.depth;
-                continue;
-            }
-            float sum = 0.0f;  // centroid component on `axis`, folded in element order
-            for (uint32_t e : it.elems) sum = sum + 0.5f * (rs[e].lo[axis] + rs[e].hi[axis]);
-            const float split = sum / (float)it.elems.size();
-            std::vector<uint32_t> low, high;
-            for (uint32_t e : it.elems) {
-                if (rs[e].hi[axis] >= split) high.push_back(e);
-                if (rs[e].lo[axis] <= split) low.push_back(e);
-            }
-            const uint32_t child = (uint32_t)kt->nodes.size();
-            if (child + 2 >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
-            std::memcpy(&kt->nodes[it.node].a, &split, 4);
-            kt->nodes[it.node].b = (child << 2) | axis;
-            kt->nodes.push_back(rt_kd_node{0, 0});
-            kt->nodes.push_back(rt_kd_node{0, 0});
-            std::vector<uint32_t>().swap(it.elems);
-            q.push_back(Item{child, it.depth + 1, std::move(low)});
-            q.push_back(Item{child + 1, it.depth + 1, std::move(high)});
-        }
+        // each element's Aabb centroid 0.5 * (lo + hi) per axis (Aabb::centroid, the value
+        // kdtree.rs:113 sums), computed once with the same f32 operations
+        std::vector<float> cen(3 * rs.size());
+        for (size_t e = 0; e < rs.size(); ++e)
+            for (int a = 0; a < 3; ++a) cen[3 * e + a] = 0.5f * (rs[e].lo[a] + rs[e].hi[a]);
+        // The top STOP levels are built here; the subtrees below them, independent of each other,
+        // on a few threads (RT_KD_THREADS, default up to 8; 1: all on this thread).  The merge
+        // renumbers everything breadth first, so the tree is byte-identical either way.
+        unsigned n_thr = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char* e = std::getenv("RT_KD_THREADS")) n_thr = (unsigned)std::max(1, std::atoi(e));
+        if (root.size() < 4096) n_thr = 1;
+        const uint32_t STOP = n_thr > 1 ? 4u : UINT32_MAX;
+        SubTree top;
+        std::vector<Frontier> frontier;
+        build_subtree(rs, cen, std::move(root), 0, max_depth, STOP, &top, n_thr > 1 ? &frontier : nullptr);
+        std::vector<SubTree> subs(frontier.size());
+        std::atomic<uint32_t> next{0};
+        auto work = [&]() {
+            for (uint32_t k; (k = next.fetch_add(1)) < frontier.size();)
+                build_subtree(rs, cen, std::move(frontier[k].elems), frontier[k].depth, max_depth, 0, &subs[k], nullptr);
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < n_thr && t < frontier.size(); ++t) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+        max_leaf_depth = top.max_leaf_depth;
+        for (const SubTree& t : subs) max_leaf_depth = std::max(max_leaf_depth, t.max_leaf_depth);
+        if ((st = merge_bfs(top, subs, kt))) { delete kt; return st; }
     }
     kt->nodes = relayout_blocked(kt->nodes);
     if (kt->nodes.size() >= (1u << 30)) { delete kt; return RT_ERR_OOM; }

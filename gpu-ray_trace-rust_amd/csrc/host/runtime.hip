@@ -7,12 +7,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -256,8 +258,21 @@ static void destroy_ctx(rt_ctx* c) {
     delete c;
 }
 
+// RT_CREATE_TIMING=1: rt_create prints the wall time of its phases to stderr (tools/host_rates.py).
+struct PhaseClock {
+    bool on = std::getenv("RT_CREATE_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "rt_create %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* cam,
                        const rt_render_info* info, const rt_kd_tree* tree_in) {
+    PhaseClock pc;
     if (info->width == 0 || info->height == 0) return set_err(c, RT_ERR_INVALID_ARG, "empty frame");
     if ((uint64_t)info->width * info->height >= (1ull << 31))
         return set_err(c, RT_ERR_INVALID_ARG, "frame too large");
@@ -265,6 +280,24 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     std::vector<Renderable> rs;
     int st = gather_renderables(scene, &rs);
     if (st) return set_err(c, st, "invalid scene description");
+
+    // The 8-bit texel pool is checked and packed (pack_texels_u8) on a thread of its own while
+    // the KD tree is built and the scene flattened: a380's 44 M texels take ~40 ms.
+    std::vector<DevTex> texs(scene->n_textures);
+    uint64_t texel_count = 0;
+    for (uint32_t i = 0; i < scene->n_textures; ++i) {
+        const rt_texture& tx = scene->textures[i];
+        if (!tx.rgb || !tx.width || !tx.height) return set_err(c, RT_ERR_INVALID_ARG, "empty texture");
+        if (texel_count + (uint64_t)tx.width * tx.height >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "texture pool too large");
+        texs[i] = DevTex{(uint32_t)texel_count, tx.width, tx.height, 0};
+        texel_count += (uint64_t)tx.width * tx.height;
+    }
+    std::vector<uint32_t> t8;
+    bool t8_ok = false;
+    std::thread packer;
+    if (texel_count && !std::getenv("RT_TEXELS_F32"))
+        packer = std::thread([&] { t8_ok = pack_texels_u8(scene, texs, texel_count, &t8); });
+    struct Join { std::thread& t; ~Join() { if (t.joinable()) t.join(); } } join{packer};
 
     rt_kd_tree* built = nullptr;
     const rt_kd_tree* tree = tree_in;
@@ -274,6 +307,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         tree = built;
     }
     struct Guard { rt_kd_tree* t; ~Guard() { rt_kd_free(t); } } guard{built};
+    pc.mark("kd_build");
 
     if (tree->max_leaf_depth > (uint32_t)MAX_STACK)
         return set_err(c, RT_ERR_UNSUPPORTED, "KD tree deeper than the device traversal stack");
@@ -287,46 +321,58 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         }
     }
 
-    // device refs: renderable index -> (kind, index of kind)
-    std::vector<uint32_t> refs(tree->n_refs);
-    for (uint32_t i = 0; i < tree->n_refs; ++i) {
-        uint32_t ri = tree->refs[i];
-        if (ri >= rs.size() || !rs[ri].has_aabb) return set_err(c, RT_ERR_INVALID_ARG, "bad leaf ref");
-        uint32_t kind = rs[ri].kind == RT_KIND_SPHERE ? K_SPHERE : (rs[ri].kind == RT_KIND_FREE_TRI ? K_FREE_TRI : K_MESH_TRI);
-        const uint32_t base = kind == K_SPHERE ? 0u : (kind == K_FREE_TRI ? scene->n_spheres
-                                                                          : scene->n_spheres + scene->n_free_tris);
-        refs[i] = (kind << REF_KIND_SHIFT) | (base + rs[ri].index);  // pool index (DevScene::prim4)
-    }
     std::vector<uint2> nodes(tree->n_nodes);
     for (uint32_t i = 0; i < tree->n_nodes; ++i) nodes[i] = make_uint2(tree->nodes[i].a, tree->nodes[i].b);
     // Leaves with identical ref lists share one copy.  A primitive that straddles many splits
     // is copied into every leaf it overlaps (kdtree.rs:119-127), so neighbouring leaves often
     // hold the same list: biplane's 5.48 M refs are 0.66 M distinct-list refs, spaceship's 3.81 M
-    // are 0.14 M, which then fit in L2.  Lists keep their order, so ties resolve as before.
+    // are 0.14 M, which then fit in L2.  Lists keep their order, so ties resolve as before.  An
+    // open-addressing table keyed on a hash of the list (the lists compared on a hash match).
+    std::vector<uint32_t> refs;  // the packed lists, then converted to device refs below
     {
-        std::unordered_map<std::string, uint32_t> seen;
-        std::vector<uint32_t> packed;
-        packed.reserve(refs.size() / 4);
+        const uint32_t* tr = tree->refs;
+        size_t n_leaf = 0;
+        for (const uint2& n : nodes) n_leaf += (n.y & 3u) == RT_KD_LEAF;
+        size_t cap = 16;
+        while (cap < 2 * n_leaf) cap <<= 1;
+        struct Entry { uint64_t h; uint32_t at, len; };
+        std::vector<Entry> table(cap, Entry{0, UINT32_MAX, 0});
+        refs.reserve(tree->n_refs / 4 + 16);
         for (uint2& n : nodes) {
             if ((n.y & 3u) != RT_KD_LEAF) continue;
             if (n.x == 0) {  // an empty leaf points at the start of the packed list: its old
                 n.y = RT_KD_LEAF;  // offset may lie past the end of it (no read needs it anyway)
                 continue;
             }
-            const uint32_t off = n.y >> 2;
-            std::string key(reinterpret_cast<const char*>(refs.data() + off), 4 * (size_t)n.x);
-            auto it = seen.find(key);
-            uint32_t at;
-            if (it != seen.end()) {
-                at = it->second;
-            } else {
-                at = (uint32_t)packed.size();
-                packed.insert(packed.end(), refs.begin() + off, refs.begin() + off + n.x);
-                seen.emplace(std::move(key), at);
+            const uint32_t off = n.y >> 2, len = n.x;
+            uint64_t h = 0x9e3779b97f4a7c15ull ^ len;
+            for (uint32_t k = 0; k < len; ++k) h = (h ^ tr[off + k]) * 0xff51afd7ed558ccdull, h ^= h >> 29;
+            size_t i = h & (cap - 1);
+            uint32_t at = UINT32_MAX;
+            for (;; i = (i + 1) & (cap - 1)) {
+                const Entry& e = table[i];
+                if (e.at == UINT32_MAX) break;
+                if (e.h == h && e.len == len && std::memcmp(refs.data() + e.at, tr + off, 4 * (size_t)len) == 0) {
+                    at = e.at;
+                    break;
+                }
+            }
+            if (at == UINT32_MAX) {
+                at = (uint32_t)refs.size();
+                refs.insert(refs.end(), tr + off, tr + off + len);
+                table[i] = Entry{h, at, len};
             }
             n.y = (at << 2) | RT_KD_LEAF;
         }
-        refs.swap(packed);
+    }
+    // device refs: renderable index -> (kind, index of kind)
+    for (uint32_t& ref : refs) {
+        const uint32_t ri = ref;
+        if (ri >= rs.size() || !rs[ri].has_aabb) return set_err(c, RT_ERR_INVALID_ARG, "bad leaf ref");
+        uint32_t kind = rs[ri].kind == RT_KIND_SPHERE ? K_SPHERE : (rs[ri].kind == RT_KIND_FREE_TRI ? K_FREE_TRI : K_MESH_TRI);
+        const uint32_t base = kind == K_SPHERE ? 0u : (kind == K_FREE_TRI ? scene->n_spheres
+                                                                          : scene->n_spheres + scene->n_free_tris);
+        ref = (kind << REF_KIND_SHIFT) | (base + rs[ri].index);  // pool index (DevScene::prim4)
     }
     // Leading sphere refs of every leaf (device_scene.h LEAF_LEAD_SHIFT): the general kernel
     // tests them per lane and leaves only triangles to the wave's cooperative passes.
@@ -373,8 +419,10 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         ftri_mat[i] = make_mat(t.mat, t.rgb);
     }
 
+    pc.mark("refs_dedupe_spheres");
     MeshFlat mf;
     if ((st = flatten_meshes(scene, &mf))) return set_err(c, st, "invalid mesh description");
+    pc.mark("flatten_meshes");
     if (mf.tris.size() >= (1u << 30)) return set_err(c, RT_ERR_INVALID_ARG, "too many mesh triangles");
     std::vector<DevPrim> prims(mf.prims.size());
     for (size_t i = 0; i < prims.size(); ++i) {
@@ -401,16 +449,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         return o;
     };
 
-    // texel pool: every scene texture, f32 RGB, in rt_scene_desc order
-    std::vector<DevTex> texs(scene->n_textures);
-    uint64_t texel_count = 0;
-    for (uint32_t i = 0; i < scene->n_textures; ++i) {
-        const rt_texture& tx = scene->textures[i];
-        if (!tx.rgb || !tx.width || !tx.height) return set_err(c, RT_ERR_INVALID_ARG, "empty texture");
-        if (texel_count + (uint64_t)tx.width * tx.height >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "texture pool too large");
-        texs[i] = DevTex{(uint32_t)texel_count, tx.width, tx.height, 0};
-        texel_count += (uint64_t)tx.width * tx.height;
-    }
 
     DevScene& d = c->sc;
     std::memset(&d, 0, sizeof(d));
@@ -432,6 +470,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
 
     HIPCHK(c, hipSetDevice(c->device));
+    pc.mark("host_arrays");
     for (Slot& sl : c->slot) {
         HIPCHK(c, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&sl.fold_done, hipEventDisableTiming));
@@ -440,6 +479,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     c->stream = c->slot[0].stream;
     HIPCHK(c, hipEventCreateWithFlags(&c->caller_ev, hipEventDisableTiming));
     HIPCHK(c, hipEventCreate(&c->win_end_ev));
+    pc.mark("streams_events");
     if ((st = upload(c, nodes, &d.nodes))) return st;
     if ((st = upload(c, elem_refs, &d.elem_refs))) return st;
     if ((st = upload(c, emit, &d.emit))) return st;
@@ -476,8 +516,10 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         // biplane 453 -> 151 MB, a380 525 -> 175 MB, under the 256 MB Infinity Cache) and decoded
         // on the device bit for bit.  Any other value keeps the f32 pool, uploaded straight from
         // the caller's arrays.
-        std::vector<uint32_t> t8;
-        if (!std::getenv("RT_TEXELS_F32") && pack_texels_u8(scene, texs, texel_count, &t8)) {
+        pc.mark("uploads");
+        if (packer.joinable()) packer.join();
+        pc.mark("texel_check_pack (joined)");
+        if (t8_ok) {
             void* p = nullptr;
             if (hipMalloc(&p, sizeof(uint32_t) * texel_count) != hipSuccess) return set_err(c, RT_ERR_OOM, "hipMalloc failed");
             c->allocs.push_back(p);
@@ -495,6 +537,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
             d.texels = static_cast<const float*>(p);
         }
     }
+    pc.mark("texel_upload");
     if ((st = upload(c, texs, &d.tex))) return st;
     if ((st = upload(c, mtri, &d.mtri))) return st;
     if ((st = upload(c, prims, &d.prims))) return st;
@@ -561,6 +604,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.debug_single_ray = info->debug_single_ray ? 1u : 0u;
     d.seed = info->seed;
 
+    pc.mark("mesh_uploads");
     const size_t npix = (size_t)info->width * info->height;
     if (hipMalloc(&c->accum, npix * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "accumulator alloc failed");
     HIPCHK(c, hipMemset(c->accum, 0, npix * sizeof(float4)));
@@ -568,6 +612,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     hipDeviceProp_t prop;
     HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
     c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
+    pc.mark("accum_props");
     c->n_cu = (uint32_t)prop.multiProcessorCount;
     if (const char* e = std::getenv("RT_SCHED")) {
         if (!std::strcmp(e, "direct")) c->sched = 1;

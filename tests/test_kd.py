@@ -70,3 +70,21 @@ def test_single_and_empty_scenes(oracle):
     sc = scheme.load(one)
     kd = compare(sc, 17, oracle)
     assert len(kd.canonical_dfs()[0]) == 1 and kd.n_refs == 1
+
+
+@pytest.mark.parametrize("name", ["walled", "biplane", "spaceship_r1", "a380", "triangles"])
+def test_parallel_build_is_byte_identical(monkeypatch, name):
+    """rt_kd_build builds the subtrees below its top levels on several threads and renumbers the
+    whole tree breadth first: the node and ref arrays equal the single-threaded build's (the
+    sequential breadth-first numbering) byte for byte."""
+    from rt_amd import render
+
+    sc = load_scene(name)
+    depth = int(sc.info.kd_tree_depth)
+    monkeypatch.setenv("RT_KD_THREADS", "1")
+    one = render.KdTree(sc.desc, depth)
+    monkeypatch.setenv("RT_KD_THREADS", "8")
+    par = render.KdTree(sc.desc, depth)
+    assert np.array_equal(one.nodes, par.nodes)
+    assert np.array_equal(one.refs, par.refs)
+    assert one.max_leaf_depth == par.max_leaf_depth and np.array_equal(one.bounds, par.bounds)

@@ -34,13 +34,22 @@ def rt_render_rate(name, spp, calls, **kw):
 def to_target_rate(name, spp, batch, **kw):
     sc = load_scene(name, **kw)
     w, h = int(sc.info.width), int(sc.info.height)
+    render.render_to_target(sc, 0, batch)  # first-touch costs of the process, untimed
+    t0 = time.perf_counter()
+    render.render_to_target(sc, 0, batch)  # zero batches: rt_create (KD build, uploads) + rt_destroy
+    setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    with render.Context(sc):
+        pass
+    create = time.perf_counter() - t0
     t0 = time.perf_counter()
     img = render.render_to_target(sc, spp, batch)
     dt = time.perf_counter() - t0
     assert img.shape == (h, w, 4)
     return {"call": "rt_render_to_target (scene upload + KD build + every batch + RGBA8 readbacks)",
             "scene": name, "pixels": w * h, "spp": spp, "batch": batch, "seconds": round(dt, 3),
-            "Msamples_s": round(w * h * spp / dt / 1e6, 1)}
+            "Msamples_s": round(w * h * spp / dt / 1e6, 1), "setup_s": round(setup, 3),
+            "rt_create_s": round(create, 3)}
 
 
 for r in (rt_render_rate("walled", 1000, 5),
