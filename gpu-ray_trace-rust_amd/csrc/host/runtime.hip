@@ -648,9 +648,12 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const unsigned long v = std::strtoul(e, nullptr, 10);
         d.restart = v > 2 ? 1u : (uint32_t)v;
     }
-    // Overlapped launches pay off where the drain tail is long (mesh scenes: 8-10 ms per launch,
-    // DESIGN.md §8); the sphere-only kernel's is ~0.4 ms.  RT_PIPELINE=0/1 overrides.
-    c->overlap = !d.spheres_only;
+    // Overlapped launches pay off while a launch's drain tail is a sizeable share of it: mesh
+    // launches (8-10 ms tails) and small sphere-only ones — walled's ~0.4 ms tail on
+    // one rank's 90 M-sample share at N = 8 (9 ms): +3% overlapped, while at 180 M it is neutral
+    // and at 360 / 720 M a fold beside the next trace grid costs 1%.  enqueue_queue overlaps
+    // launches of at most overlap_max_items (2^27) samples.  RT_PIPELINE=0/1/2 overrides.
+    c->overlap = true;
     if (const char* e = std::getenv("RT_PIPELINE_SLOTS")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 2 && v <= (unsigned long)N_SLOTS) c->n_slots = (uint32_t)v;

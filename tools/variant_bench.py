@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--scene", default="walled")
     ap.add_argument("--spp", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
     ap.add_argument("names", nargs="+")
     a = ap.parse_args()
     import torch  # noqa: F401  (owns the HIP runtime)
@@ -34,7 +36,8 @@ def main():
         path = (os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "librt_amd.so") if lname == "main" else
                 os.path.join(ROOT, "gpu-ray_trace-rust_amd", "lib", "variants", f"librt_{lname}.so"))
         lib = abi.load_library(path)
-        loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"), lib=lib)
+        loaded = scheme.load(sch, assets_root=os.path.join(ROOT, "assets_pack"), lib=lib, width=a.width,
+                             height=a.height)
         ctxs[n] = (render.Context(loaded, lib=lib), loaded)
         for k, v in saved.items():
             if v is None:
