@@ -42,3 +42,10 @@ def test_libm_restatement_exhaustive_cpu():
     4.2e9 inputs, bit for bit (about 10 s on 8 cores)."""
     r = _run("check_libm", "full", timeout=600)
     assert r["sincos_all_floats_pm2pi"][1] == 0 and r["powf5_all_floats"][1] == 0, r
+
+
+def test_powf5_every_float_cpu():
+    """powf(x, 5) on all 2^32 float bit patterns (negative, subnormal, zero, inf, NaN and the
+    overflow / underflow range included), bit for bit against glibc (about 10 s on 8 cores)."""
+    r = _run("check_libm", "pow_all", timeout=600)
+    assert r["powf5_every_float"] == [1 << 32, 0, "0x00000000"], r
