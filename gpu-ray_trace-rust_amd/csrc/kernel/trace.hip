@@ -969,9 +969,10 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             VC(0, 1);
             pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
-                VC(0, RT_PAIR_FETCH ? 2 : 1);
-                // RT_PAIR_FETCH: both children (adjacent, 16 B) are loaded before this node's
-                // decision, so the next level's fetch overlaps the decision's arithmetic
+                VC(0, 1);
+                // RT_PAIR_FETCH: both children (adjacent, 16 B: one global_load_dwordx4) are
+                // loaded before this node's decision, so the next level's fetch overlaps the
+                // decision's arithmetic
                 const uint32_t cpair = nd.y >> 2;
                 uint4 pair = make_uint4(0u, 0u, 0u, 0u);
                 if (RT_PAIR_FETCH) {
