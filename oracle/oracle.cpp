@@ -76,7 +76,8 @@ static inline M3 mul(const M3& a, const M3& b) {
 static thread_local rt_rng_state g_rng;
 // Shading-mix instrumentation (counted renders only, tools/min_insts.py): per continued ray by
 // branch, the draws, and the Russian-roulette draws.
-enum { MIX_SPEC, MIX_DIFF, MIX_DIFFSPEC_DIFF, MIX_DIFFSPEC_SPEC, MIX_DIELECTRIC, MIX_RR, MIX_DRAWS, MIX_MESH, MIX_N };
+enum { MIX_SPEC, MIX_DIFF, MIX_DIFFSPEC_DIFF, MIX_DIFFSPEC_SPEC, MIX_DIELECTRIC, MIX_RR, MIX_DRAWS, MIX_MESH,
+       MIX_POSDISC, MIX_N };
 static thread_local uint64_t* g_mix = nullptr;
 #define MIX(i) do { if (g_mix) g_mix[i]++; } while (0)
 static std::mutex g_mix_mu;
@@ -280,6 +281,14 @@ struct Sphere final : Element {
         hr->l = f;
         hr->pos = ray.o + ray.d * f;
         return true;
+    }
+    // tools/min_insts.py's event count: whether this ray's line meets the sphere (thing2 > 0,
+    // the same f32 steps as intersect), i.e. whether a brute-force closest hit needs its roots
+    bool disc_positive(const Ray& ray) const {
+        V3 oc = ray.o - mk(s->c);
+        float dir = dot(ray.d, oc);
+        float consts = dot(oc, oc) - s->r * s->r;
+        return dir * dir - consts > 0.0f;
     }
     bool give_aabb(Aabb* b) const override {  // :106-114
         for (int a = 0; a < 3; ++a) { b->lo[a] = s->c[a] - s->r; b->hi[a] = s->c[a] + s->r; }
@@ -862,6 +871,9 @@ static V3 radiance_forward(Ray ray, const Scene& s, const RadInfo& ri) {
     V3 p_T = mk(0.f, 0.f, 0.f);
     for (int depth = 0;; ++depth) {
         COUNT(segments, 1);
+        if (g_mix)  // spheres whose roots a brute-force closest hit computes (min_insts.py)
+            for (const Element* e : s.renderables)
+                if (const Sphere* sp = dynamic_cast<const Sphere*>(e)) { if (sp->disc_positive(ray)) MIX(MIX_POSDISC); }
         Closest c = s.kd.closest(ray);
         if (pending) {
             L = L + cmul(p_T, dls_contrib(s, p_idx, c.found ? (int)c.elem_idx : -1, p_hi, p_ray));
@@ -1137,8 +1149,9 @@ extern "C" void oracle_refract(const float d[3], const float n[3], float n_out, 
 
 // Shading mix of the counted renders since the last reset (continued rays by material branch:
 // spec, diff, diffspec->diff, diffspec->spec, dielectric; Russian-roulette draws; all draws;
-// mesh continues), for tools/min_insts.py.
-extern "C" void oracle_mix_counts(uint64_t out[8], int reset) {
+// mesh continues; forward-order segments' spheres with a positive discriminant), for
+// tools/min_insts.py.
+extern "C" void oracle_mix_counts(uint64_t out[9], int reset) {
     std::lock_guard<std::mutex> lk(g_mix_mu);
     for (int i = 0; i < MIX_N; ++i) {
         out[i] = g_mix_total[i];

@@ -55,7 +55,7 @@ int oracle_render_ex(const rt_scene_desc* scene, const rt_camera* cam, const rt_
 /* Shading mix of the counted renders (counts != NULL) since the last reset: continued rays by
  * material branch {spec, diff, diffspec->diff, diffspec->spec, dielectric}, Russian-roulette
  * draws, all draws, mesh continues. */
-void oracle_mix_counts(uint64_t out[8], int reset);
+void oracle_mix_counts(uint64_t out[9], int reset);
 
 /* KdTree::build (kdtree.rs:26-56,107-137) as a pointer tree, then a canonical depth-first
  * pre-order dump: per node {is_leaf, axis, split bits | leaf count, first ref}; refs in

@@ -113,11 +113,12 @@ def mesh_normal_transforms(desc, n_tris):
     return out[:k]
 
 
-MIX_FIELDS = ("spec", "diff", "diffspec_diff", "diffspec_spec", "dielectric", "rr_draws", "draws", "mesh")
+MIX_FIELDS = ("spec", "diff", "diffspec_diff", "diffspec_spec", "dielectric", "rr_draws", "draws", "mesh",
+              "sphere_disc_positive")
 
 
 def mix_counts(reset=True):
     """Shading mix of the counted renders (render(..., counts=True)) since the last reset."""
-    out = (C.c_uint64 * 8)()
+    out = (C.c_uint64 * len(MIX_FIELDS))()
     lib().oracle_mix_counts(out, int(reset))
     return dict(zip(MIX_FIELDS, (int(v) for v in out)))

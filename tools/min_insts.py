@@ -8,10 +8,11 @@ restatements their polynomial and reduction steps, 64-bit integer work its 32-bi
 address arithmetic, loop control, the exactness guards and the queue bookkeeping are not in the
 floor.  The per-event counts come from the oracle's instrumented render of the reference algorithm
 on the bench's scene (every 16th pixel in x and y, 16 spp, SURVEY.md §8d's grid): segments,
-sphere hits, continued rays by material branch, Russian-roulette draws and all draws.  The
-closest-hit floor is the device algorithm's (closest_small: every sphere's discriminant, the
-roots of the hit sphere, the in_return_leaf decision), which returns the reference's sphere and
-length exactly; the reference's own traversal costs far more (507 node steps).
+sphere hits, spheres whose discriminant is positive, continued rays by material branch,
+Russian-roulette draws and all draws.  The closest-hit floor is the device algorithm's
+(closest_small: every sphere's discriminant, the roots of every sphere the ray's line meets,
+the in_return_leaf decision), which returns the reference's sphere and length exactly
+(DESIGN.md §5); the reference's own traversal costs far more (507 node steps).
 
 Usage: python tools/min_insts.py [scene] -> profiles/min_insts_<scene>.json"""
 import json
@@ -37,10 +38,13 @@ OPS = {
     # per sphere and segment: sphere_disc, o - c (3), two dots (10), - r^2, dir^2 - consts (2),
     # the thing2 > 0 test
     "sphere_disc": 17,
-    # per segment that hits: the hit sphere's roots (sqrt, -dir, two adds, l1 > 0, select,
-    # l >= HIT_MIN, l < best, two selects) 10; ray_axes (3 clamps of 3, 3 reciprocals) 12; the
-    # root slab test 22; in_return_leaf (3 axes x 10, the descent floor 3) 33
-    "hit_segment": 10 + 12 + 22 + 33,
+    # per sphere whose discriminant is positive (the ray's line meets it): its roots and the
+    # running minimum (sqrt, -dir, two adds, l1 > 0, select, l >= HIT_MIN, l < best, two
+    # selects); the closest hit needs every such sphere's length
+    "sphere_roots": 10,
+    # per segment that hits: ray_axes (3 clamps of 3, 3 reciprocals) 12; the root slab test 22;
+    # in_return_leaf (3 axes x 10, the descent floor 3) 33
+    "hit_segment": 12 + 22 + 33,
     # per sphere hit: hit_info (perfect 6, normalize(perfect - c) 12, pos 6), emission 6, T *= rgb
     # * p 6, d.n 5, the mirror direction 9
     "hit": 24 + 6 + 6 + 5 + 9,
@@ -72,13 +76,15 @@ def main(scene="walled"):
     n = c["samples"]
     per = {"segments": c["segments"] / n, "hits": c["hits"] / n, "draws": m["draws"] / n,
            "diff": m["diff"] / n, "diffspec": (m["diffspec_diff"] + m["diffspec_spec"]) / n,
-           "spec": m["spec"] / n, "dielectric": m["dielectric"] / n, "rr_draws": m["rr_draws"] / n}
+           "spec": m["spec"] / n, "dielectric": m["dielectric"] / n, "rr_draws": m["rr_draws"] / n,
+           "sphere_disc_positive": m["sphere_disc_positive"] / n}
     n_sph = int(sc.desc.n_spheres)
     parts = {
         "sample": OPS["sample"],
         "draws": OPS["draw"] * per["draws"],
         "segments": OPS["segment"] * per["segments"],
         "sphere_discriminants": OPS["sphere_disc"] * n_sph * per["segments"],
+        "sphere_roots": OPS["sphere_roots"] * per["sphere_disc_positive"],
         "hit_segments": OPS["hit_segment"] * per["hits"],
         "hits": OPS["hit"] * per["hits"],
         "diffuse": OPS["diff"] * (per["diff"] + m["diffspec_diff"] / n),
