@@ -135,3 +135,29 @@ def test_hw_queues_report():
     import json
     r = json.loads(out.stdout)
     assert r == {"value": "12", "source": "rt_amd", "hip_started_before_import": False}
+
+
+def test_committed_counters_belong_to_this_build():
+    """bench.py prices each config's roofline with the committed rocprofv3 counters of the SAME
+    device code (profiles/*_counters.json, keyed on the .hip_fatbin hash): every bench config's
+    counters must carry the build id of the library this tree builds, or the round's bench line
+    would report `null` fractions.  A kernel change therefore needs a re-profile
+    (tools/gpu_profile_all.sh) before it is committed."""
+    import glob
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+    from rt_amd import abi
+
+    bid = abi.kernel_build_id()
+    found = {}
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*_counters.json")):
+        d = json.load(open(p))
+        if d.get("build_id") == bid:
+            found.setdefault(d.get("scene"), set()).add(d.get("samples_per_launch"))
+    # the bench's configs (bench.py CONFIGS and the walled headline) at their launch shapes
+    want = {"walled": 720_000_000, "a380": 720_000, "biplane": 7_200_000, "spaceship_r1": 419_430_400,
+            "triangles": 7_200_000}
+    missing = {s: n for s, n in want.items() if n not in found.get(s, set())}
+    assert not missing, f"no committed counters of build {bid} for {missing}: re-profile"
