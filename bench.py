@@ -47,15 +47,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
 
 # The launch pipeline's slots each want their own HIP hardware queue (launch
-# pipeline): this benchmark chooses GPU_MAX_HW_QUEUES = 12 before HIP starts unless the caller
+# pipeline): this benchmark chooses GPU_MAX_HW_QUEUES = 16 before HIP starts unless the caller
 # asked for at least that, and reports what it ran with (rt_amd itself keeps explicit values).
 HW_QUEUES_BEFORE = os.environ.get("GPU_MAX_HW_QUEUES")
 try:
     _q = int(HW_QUEUES_BEFORE or "0")
 except ValueError:
     _q = 0
-if _q < 12:
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
+if _q < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import rt_amd  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec

@@ -41,14 +41,29 @@ static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 // buffer, item counter and traversal-stack scratch: launch i + 1 starts while launch i drains
 // (its last paths finish on a few lanes), and only the folds, which update the shared
 // accumulators and the output, are chained in order by events.  A mesh launch's drain tail is
-// ~8-10 ms; a 1-spp a380 launch holds ~2 ms of work, so small launches need more of them in
-// flight to cover one tail: 8 slots for launches of up to 2^21 samples, else 2.  The slots'
-// streams overlap only on separate hardware queues: with HIP's default GPU_MAX_HW_QUEUES = 4,
-// a380 at 1 spp ran 187 Msamples/s whatever the slots; with 8 queues 2 / 4 / 6 slots ran
-// 137 / 229 / 272, with 12 queues and 8 slots 288 (rt_amd sets 12 before HIP starts).  Larger
-// launches: 2 slots (12 queues, biplane at 10 spp 590 / 587 / 569 with 2 / 3 / 4 slots).
-// RT_PIPELINE_SLOTS (2-8) fixes the count.
-constexpr int N_SLOTS = 8;
+// ~8-10 ms; a 1-spp a380 launch holds ~2 ms of work, so small launches (up to 2^21 samples) need
+// many of them in flight to cover one tail, larger ones 2 slots (biplane at 10 spp 590 / 587 /
+// 569 with 2 / 3 / 4).  The slots' streams overlap only on separate hardware queues: HIP maps
+// streams onto GPU_MAX_HW_QUEUES queues (4 by default) as they are created, and streams sharing
+// a queue run in order (a380 at 1 spp: 4 queues 187 Msamples/s whatever the slots; 8 queues with
+// 2 / 4 / 6 slots 137 / 229 / 272; 12 queues, 8 slots 288-356).  So a context creates a slot's
+// stream on first use, and small launches use slots_for_queues(GPU_MAX_HW_QUEUES) slots: four
+// queues are left to the caller's streams (torch's, RCCL's), at most 12 slots (16 queues:
+// 12 slots; with 32 queues and 24 slots a380 fell to 183, the queues oversubscribed).
+// While the pipeline is busy, a small launch also takes only 1/grid_div of the resident grid
+// (small_grid_div): its waves then trace several items per lane, so the drain of each wave's
+// last paths, which holds its slot on the CU, is spread over more work, and more launches run
+// side by side.  a380 at 1 spp, 16 queues (round 3, tools/gpu_a380_calib.py): 8 slots, full grid
+// 356; 8 slots, 1/4 grid 370 (1/6: 350, 1/8: 318); 12 slots, 1/6 389, 1/8 400, 1/10 380;
+// biplane / spaceship launches (2 slots) lose with a smaller grid (1/2: -14% / -2%), so they keep
+// the full one.  The first launch of an idle pipeline (and every synchronous call) keeps the full
+// grid too.  RT_PIPELINE_SLOTS (2-32) and RT_QUEUE_GRID_DIV (1-64) override.
+constexpr int N_SLOTS = 32;          // slots a context holds (RT_PIPELINE_SLOTS up to this)
+static uint32_t slots_for_queues(int hw_queues) {
+    const int s = hw_queues - 4;
+    return s < 2 ? 2u : (s > 12 ? 12u : (uint32_t)s);
+}
+static uint32_t small_grid_div(uint32_t slots) { return slots >= 12 ? 8u : (slots >= 8 ? 4u : 1u); }
 constexpr uint64_t SMALL_LAUNCH_ITEMS = 1ull << 21;
 struct Slot {
     hipStream_t stream = nullptr;
@@ -102,6 +117,8 @@ struct rt_ctx {
     bool overlap = true;          // RT_PIPELINE: launch i + 1 may start during launch i's drain
     uint64_t overlap_max_items = 1ull << 27;  // ... when it has at most this many samples
     uint32_t n_slots = 0;         // RT_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
+    uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
+    uint32_t grid_div = 1;        // small launches behind a busy pipeline: 1/grid_div of the resident grid
     float last_ms = 0.f;
     std::string err;
 };
@@ -231,6 +248,19 @@ static bool pack_texels_u8(const rt_scene_desc* scene, const std::vector<DevTex>
     }
     for (auto& th : pool) th.join();
     return ok.load();
+}
+
+// A pipeline slot's stream, fold event and item counter, created on the slot's first use: HIP
+// maps streams onto its GPU_MAX_HW_QUEUES hardware queues as they are created, so a context
+// makes only the streams its launches rotate over (one for large launches, n_slots for small
+// overlapped ones) and leaves the other queues to the caller's streams.
+static int ensure_slot(rt_ctx* c, uint32_t k) {
+    Slot& sl = c->slot[k];
+    if (sl.stream) return RT_OK;
+    HIPCHK(c, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&sl.fold_done, hipEventDisableTiming));
+    if (hipMalloc(&sl.queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
+    return RT_OK;
 }
 
 static void destroy_ctx(rt_ctx* c) {
@@ -471,11 +501,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
 
     HIPCHK(c, hipSetDevice(c->device));
     pc.mark("host_arrays");
-    for (Slot& sl : c->slot) {
-        HIPCHK(c, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&sl.fold_done, hipEventDisableTiming));
-        if (hipMalloc(&sl.queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
-    }
+    if ((st = ensure_slot(c, 0))) return st;  // the others on first use (enqueue_queue)
     c->stream = c->slot[0].stream;
     HIPCHK(c, hipEventCreateWithFlags(&c->caller_ev, hipEventDisableTiming));
     HIPCHK(c, hipEventCreate(&c->win_end_ev));
@@ -658,6 +684,16 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 2 && v <= (unsigned long)N_SLOTS) c->n_slots = (uint32_t)v;
     }
+    {
+        const char* q = std::getenv("GPU_MAX_HW_QUEUES");  // what HIP read when it started
+        const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
+        c->small_slots = slots_for_queues(hwq);
+        c->grid_div = small_grid_div(c->small_slots);
+    }
+    if (const char* e = std::getenv("RT_QUEUE_GRID_DIV")) {
+        const unsigned long v = std::strtoul(e, nullptr, 10);
+        if (v >= 1 && v <= 64) c->grid_div = (uint32_t)v;
+    }
     if (const char* e = std::getenv("RT_PIPELINE")) {  // 0: never, 1: below the item limit, 2: always
         c->overlap = std::strcmp(e, "0") != 0;
         if (!std::strcmp(e, "2")) c->overlap_max_items = ~0ull;
@@ -692,7 +728,7 @@ extern "C" int rt_create(const rt_scene_desc* scene, const rt_camera* cam, const
 // Drains both pipeline slots and closes the timing window: per-launch trace durations and the
 // window's span, from its first trace launch to its last fold.
 static int sync_all(rt_ctx* c) {
-    for (Slot& sl : c->slot) HIPCHK(c, hipStreamSynchronize(sl.stream));
+    for (Slot& sl : c->slot) if (sl.stream) HIPCHK(c, hipStreamSynchronize(sl.stream));
     if (!c->pending) return RT_OK;
     c->pending = false;
     c->trace_ms = 0.f;
@@ -907,8 +943,15 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         // Overlapped launches alternate slots; a serialized one stays on the last slot's stream,
         // behind its fold, with one radiance buffer.
         const bool overlap = c->overlap && a.n_items <= c->overlap_max_items;
-        const uint32_t n_slots = c->n_slots ? c->n_slots : (a.n_items <= SMALL_LAUNCH_ITEMS ? (uint32_t)N_SLOTS : 2u);
+        const bool small = a.n_items <= SMALL_LAUNCH_ITEMS;
+        // a small launch behind a launch still running takes a share of the grid (see N_SLOTS)
+        const bool busy = c->last_fold && hipEventQuery(c->last_fold) == hipErrorNotReady;
+        const uint32_t n_slots = c->n_slots ? c->n_slots : (small ? c->small_slots : 2u);
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
+        for (uint32_t k = 0; k < (overlap ? n_slots : 1u); ++k) {
+            const int e = ensure_slot(c, overlap ? k : c->cur_slot);
+            if (e) return e;
+        }
         Slot& sl = c->slot[c->cur_slot];
         const uint64_t floats = 3 * n_out * (a.sample_count ? a.sample_count : 1);
         int st = ensure_radiance(c, sl, floats);
@@ -934,7 +977,10 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         if (a.sample_count) {
             HIPCHK(c, hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), sl.stream));
             if ((st = record_launch_event(c, true, sl.stream))) return st;
-            HIPCHK(c, launch_trace_queue(a, (uint32_t)(lanes / BLOCK), sl.stream));
+            uint32_t nb = (uint32_t)(lanes / BLOCK);
+            if (overlap && small && busy && c->grid_div > 1)
+                nb = nb / c->grid_div > (uint32_t)c->n_cu ? nb / c->grid_div : (uint32_t)c->n_cu;
+            HIPCHK(c, launch_trace_queue(a, nb, sl.stream));
             if ((st = record_launch_event(c, false, sl.stream))) return st;
         }
         if (c->last_fold && c->last_fold != sl.fold_done) HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));
@@ -1163,7 +1209,7 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
     // Batches in flight: batch i + AHEAD is enqueued before batch i is read back, each into its
     // own output buffer, so the launch pipeline's slots stay busy (a 1-spp batch holds ~2 ms of
     // work against a ~10 ms drain tail); the hook still sees every batch, in order.
-    constexpr uint32_t AHEAD = (uint32_t)N_SLOTS - 1u;
+    const uint32_t AHEAD = (npix * batch <= SMALL_LAUNCH_ITEMS ? c->small_slots : 8u) - 1u;
     const uint32_t n_batch = spp / batch;
     const uint32_t ring = std::min(AHEAD, n_batch ? n_batch - 1u : 0u) + 1u;
     std::vector<float4*> dbuf(ring, nullptr);

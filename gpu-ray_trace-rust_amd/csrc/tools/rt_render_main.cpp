@@ -50,10 +50,10 @@ int usage() {
 
 int main(int argc, char** argv) {
     // the launch pipeline's streams need their own hardware queues (rt_amd/__init__.py): at
-    // least 12, set before HIP starts
+    // least 16, set before HIP starts
     {
         const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-        if (!q || std::atoi(q) < 12) setenv("GPU_MAX_HW_QUEUES", "12", 1);
+        if (!q || std::atoi(q) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
     }
     if (argc < 2) return usage();
     std::string scheme_path = argv[1], assets = "assets_pack", out = "render_out.png";

@@ -3,14 +3,14 @@
 reached through the C ABI of include/rt_abi.h; this package only loads scenes and calls it."""
 import os
 
-# Overlapped queue launches run on up to 8 pipeline streams (runtime.hip, launch pipeline); HIP
+# Overlapped queue launches run on up to 12 pipeline streams (runtime.hip, launch pipeline); HIP
 # maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), and streams sharing a queue
-# run one after another (a380 at its batch of 1 spp: 4 queues 183, 12 queues 313 Msamples/s).
-# HIP reads the variable when it starts, so when it is unset it is set to 12 here, before the
-# first HIP call of the process; an explicit value is the caller's choice and is kept (bench.py
-# and lib/rt_render choose 12 themselves).  hw_queues() reports the value HIP started with, as
-# far as this process can tell.
-RECOMMENDED_HW_QUEUES = 12
+# run one after another (a380 at its batch of 1 spp: 4 queues 183, 12 queues 356, 16 queues with
+# 12 slots 400 Msamples/s).  HIP reads the variable when it starts, so when it is unset it is set
+# to 16 here, before the first HIP call of the process; an explicit value is the caller's choice
+# and is kept (the library then sizes its pipeline to it; bench.py and lib/rt_render choose 16
+# themselves).  hw_queues() reports the value HIP started with, as far as this process can tell.
+RECOMMENDED_HW_QUEUES = 16
 _SET_BY_RT_AMD = "GPU_MAX_HW_QUEUES" not in os.environ
 if _SET_BY_RT_AMD:
     os.environ["GPU_MAX_HW_QUEUES"] = str(RECOMMENDED_HW_QUEUES)

@@ -104,9 +104,9 @@ def test_create_without_device_fails_cleanly(rtlib, walled):
     assert st == abi.RT_ERR_NO_DEVICE and not ctx.value
 
 
-@pytest.mark.parametrize("before,after", [(None, "12"), ("4", "4"), ("16", "16"), ("junk", "junk")])
+@pytest.mark.parametrize("before,after", [(None, "16"), ("4", "4"), ("12", "12"), ("junk", "junk")])
 def test_hw_queues_set_only_when_unset(before, after):
-    """Importing rt_amd sets GPU_MAX_HW_QUEUES to 12 when it is unset (the launch pipeline's
+    """Importing rt_amd sets GPU_MAX_HW_QUEUES to 16 when it is unset (the launch pipeline's
     streams each need a hardware queue) and keeps any explicit value: that is the
     caller's choice (bench.py makes its own, and reports it)."""
     import subprocess
@@ -134,7 +134,7 @@ def test_hw_queues_report():
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     import json
     r = json.loads(out.stdout)
-    assert r == {"value": "12", "source": "rt_amd", "hip_started_before_import": False}
+    assert r == {"value": "16", "source": "rt_amd", "hip_started_before_import": False}
 
 
 def test_committed_counters_belong_to_this_build():
