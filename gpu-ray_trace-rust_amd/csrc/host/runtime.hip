@@ -64,7 +64,7 @@ static uint32_t slots_for_queues(int hw_queues) {
     return s < 2 ? 2u : (s > 12 ? 12u : (uint32_t)s);
 }
 static uint32_t small_grid_div(uint32_t slots) { return slots >= 12 ? 8u : (slots >= 8 ? 4u : 1u); }
-constexpr uint64_t SMALL_LAUNCH_ITEMS = 1ull << 21;
+constexpr uint64_t SMALL_LAUNCH_ITEMS = 1ull << 21;  // default of rt_ctx::small_items
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t fold_done = nullptr;   // this slot's last fold (its radiance buffer is free again)
@@ -118,6 +118,7 @@ struct rt_ctx {
     uint64_t overlap_max_items = 1ull << 27;  // ... when it has at most this many samples
     uint32_t n_slots = 0;         // RT_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
     uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
+    uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_SMALL_LAUNCH_ITEMS: launches this size or less are small
     uint32_t grid_div = 1;        // small launches behind a busy pipeline: 1/grid_div of the resident grid
     float last_ms = 0.f;
     std::string err;
@@ -690,6 +691,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         c->small_slots = slots_for_queues(hwq);
         c->grid_div = small_grid_div(c->small_slots);
     }
+    if (const char* e = std::getenv("RT_SMALL_LAUNCH_ITEMS")) c->small_items = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("RT_QUEUE_GRID_DIV")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->grid_div = (uint32_t)v;
@@ -943,7 +945,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         // Overlapped launches alternate slots; a serialized one stays on the last slot's stream,
         // behind its fold, with one radiance buffer.
         const bool overlap = c->overlap && a.n_items <= c->overlap_max_items;
-        const bool small = a.n_items <= SMALL_LAUNCH_ITEMS;
+        const bool small = a.n_items <= c->small_items;
         // a small launch behind a launch still running takes a share of the grid (see N_SLOTS)
         const bool busy = c->last_fold && hipEventQuery(c->last_fold) == hipErrorNotReady;
         const uint32_t n_slots = c->n_slots ? c->n_slots : (small ? c->small_slots : 2u);
@@ -1209,7 +1211,7 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
     // Batches in flight: batch i + AHEAD is enqueued before batch i is read back, each into its
     // own output buffer, so the launch pipeline's slots stay busy (a 1-spp batch holds ~2 ms of
     // work against a ~10 ms drain tail); the hook still sees every batch, in order.
-    const uint32_t AHEAD = (npix * batch <= SMALL_LAUNCH_ITEMS ? c->small_slots : 8u) - 1u;
+    const uint32_t AHEAD = (npix * batch <= c->small_items ? c->small_slots : 8u) - 1u;
     const uint32_t n_batch = spp / batch;
     const uint32_t ring = std::min(AHEAD, n_batch ? n_batch - 1u : 0u) + 1u;
     std::vector<float4*> dbuf(ring, nullptr);
