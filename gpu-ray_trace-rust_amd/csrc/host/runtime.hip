@@ -59,6 +59,8 @@ static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 // the full one.  The first launch of an idle pipeline (and every synchronous call) keeps the full
 // grid too.  RT_PIPELINE_SLOTS (2-32) and RT_QUEUE_GRID_DIV (1-64) override.
 constexpr int N_SLOTS = 32;          // slots a context holds (RT_PIPELINE_SLOTS up to this)
+// A launch's item counters: one 128-B line per shard of its items (trace.hip RT_QSHARDS, <= 32)
+constexpr size_t QUEUE_BYTES = 32 * 128;
 static uint32_t slots_for_queues(int hw_queues) {
     const int s = hw_queues - 4;
     return s < 2 ? 2u : (s > 12 ? 12u : (uint32_t)s);
@@ -260,7 +262,7 @@ static int ensure_slot(rt_ctx* c, uint32_t k) {
     if (sl.stream) return RT_OK;
     HIPCHK(c, hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&sl.fold_done, hipEventDisableTiming));
-    if (hipMalloc(&sl.queue, sizeof(uint32_t)) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
+    if (hipMalloc(&sl.queue, QUEUE_BYTES) != hipSuccess) return set_err(c, RT_ERR_OOM, "queue alloc failed");
     return RT_OK;
 }
 
@@ -977,7 +979,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         if (!overlap && c->last_fold && c->last_fold != sl.fold_done)
             HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));
         if (a.sample_count) {
-            HIPCHK(c, hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), sl.stream));
+            HIPCHK(c, hipMemsetAsync(sl.queue, 0, QUEUE_BYTES, sl.stream));
             if ((st = record_launch_event(c, true, sl.stream))) return st;
             uint32_t nb = (uint32_t)(lanes / BLOCK);
             if (overlap && small && busy && c->grid_div > 1)

@@ -165,8 +165,9 @@ struct LaunchArgs {
     uint32_t n_pix_magic;   // floor(2^32 / n_pix) (0 for n_pix = 1): item / n_pix by multiply-high
     float* radiance;
     // Queue schedule (launch_trace_queue): persistent lanes take (pixel, sample) items
-    // item = j * n_pix + o (sample j of the launch, output pixel o) from *queue in wave-sized
-    // grabs, trace them into `radiance` and fold_kernel folds them in sample order.
+    // item = j * n_pix + o (sample j of the launch, output pixel o) in wave-sized grabs from the
+    // counters of its shards (queue[k * 32], k < RT_QSHARDS: one 128-B line each, zeroed before
+    // the launch), trace them into `radiance` and fold_kernel folds them in sample order.
     uint32_t* queue;
     uint32_t n_items;       // n_pix * sample_count
     // Sphere-only queue kernel: its traversal stack in global memory, [block][stack_depth][BLOCK]

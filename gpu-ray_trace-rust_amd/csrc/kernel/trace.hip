@@ -1811,6 +1811,50 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
     return g < qmin ? qmin : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
+// The launch's items in RT_QSHARDS sub-ranges, each with its own counter (a 128-B line of
+// a.queue): every grab is one device-scope atomic, and on one counter they serialise — a cheap
+// scene's 64-item grabs (triangles.yml at 10 spp: ~112 K atomics per 1.4 ms launch) waited on it
+// for most of the launch.  A wave starts on shard blockIdx % RT_QSHARDS (blocks are dealt to the
+// 8 XCDs round-robin, so each XCD starts on its own shard) and moves to the next shard when its
+// own is exhausted; it is done when it has found every shard exhausted (counters only grow).
+// Shard boundaries are multiples of 64, so a grab (a multiple of 64, at least 64) that starts
+// inside a shard covers every lane that asks.  Which lane traces an item changes, never what
+// the item computes: bit-identical images.
+#ifndef RT_QSHARDS
+#define RT_QSHARDS 8
+#endif
+constexpr uint32_t QSHARD_STRIDE = 32;  // uint32 words between shard counters (128 B)
+static_assert(RT_QSHARDS >= 1 && RT_QSHARDS <= 32, "RT_QSHARDS: 1..32 (a.queue holds 32 lines)");
+__device__ __forceinline__ uint32_t qshard_begin(uint32_t n_items, uint32_t k) {
+    if (k == 0) return 0u;
+    const uint64_t b = ((uint64_t)n_items * k / RT_QSHARDS + 63u) & ~63ull;
+    return b < n_items ? (uint32_t)b : n_items;
+}
+// One grab of `grab` items for the wave (wave-uniform; `lane_op` is the lane that issues the
+// atomic): from shard qk, moving on while shards are exhausted.  Returns [*base, *end) (end the
+// shard's end, so the pool is clipped to it); *exhausted when every shard is.
+__device__ __forceinline__ void qgrab(const LaunchArgs& a, uint32_t grab, uint32_t lane_op, uint32_t& qk,
+                                      uint32_t& q_seen, bool& exhausted, uint32_t* base, uint32_t* end) {
+    const uint32_t lane = __lane_id();
+    for (;;) {
+        const uint32_t b = qshard_begin(a.n_items, qk), e = qshard_begin(a.n_items, qk + 1);
+        uint32_t b0 = 0;
+        if (lane == lane_op) b0 = atomicAdd(a.queue + qk * QSHARD_STRIDE, grab);
+        const uint32_t off = __builtin_amdgcn_readfirstlane(__shfl(b0, lane_op));
+        if (off < e - b) {
+            *base = b + off;
+            *end = e;
+            return;
+        }
+        if (++q_seen >= RT_QSHARDS) {  // every shard exhausted: no items
+            exhausted = true;
+            *base = *end = a.n_items;
+            return;
+        }
+        qk = qk + 1 == RT_QSHARDS ? 0u : qk + 1;
+    }
+}
+
 // Path starts in batches (RT_START_BATCH, the sphere-only kernel, cameras without a lens).  A
 // start is the item's pixel, the stream key, the SplitMix64 round and camera_ray's two jitter
 // draws.  Made by the idle lanes alone, it ran at the width of the lanes that had just finished,
@@ -1868,7 +1912,10 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint32_t grab = grab_size<GEN>(a.n_items, n_waves);
+    uint32_t grab = grab_size<GEN>(a.n_items / RT_QSHARDS, (n_waves + RT_QSHARDS - 1) / RT_QSHARDS);
+    uint32_t qk = blockIdx.x % RT_QSHARDS, q_seen = 0;  // wave-uniform: its shard, shards found exhausted
+    bool q_out = false;                                 // wave-uniform: every shard exhausted
+    const uint32_t shard_waves = (n_waves + RT_QSHARDS - 1) / RT_QSHARDS;
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
@@ -1903,16 +1950,18 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             };
             if (idle && r < st_n) take(st_pos + r);  // before the next batch overwrites them
             if (n > st_n) {
-                if (pool == pool_end) {  // grabs are multiples of 64: a batch never spans two
-                    uint32_t b0 = 0;
-                    if (lane == 0) b0 = atomicAdd(a.queue, grab);
-                    pool = __builtin_amdgcn_readfirstlane(b0);
-                    pool_end = pool + grab;
-                    grab = grab_size<GEN>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+                if (pool >= pool_end) {  // grabs and shards are multiples of 64: a batch spans neither
+                    uint32_t qe = a.n_items;  // (but the last shard may end inside its last batch)
+                    pool = pool_end = a.n_items;  // past the items: START_NONE entries
+                    if (!q_out) {
+                        qgrab(a, grab, 0u, qk, q_seen, q_out, &pool, &qe);
+                        pool_end = pool + grab < qe ? pool + grab : qe;
+                        grab = grab_size<GEN>(qe - pool_end, shard_waves);
+                    }
                 }
                 __builtin_amdgcn_wave_barrier();
-                make_start(a, sc, pool + lane, lane, e);
-                pool += 64u;
+                make_start(a, sc, pool < pool_end ? pool + lane : a.n_items, lane, e);
+                if (pool < pool_end) pool += 64u;
                 __builtin_amdgcn_wave_barrier();
                 if (idle && r >= st_n) take(r - st_n);
                 st_pos = n - st_n;
@@ -1923,7 +1972,9 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             }
             if (idle) {
                 if (v[5] == START_NONE) {
-                    done = true;
+                    // past the items: done once every shard is exhausted, else the lane takes
+                    // the next batch's entry (the last shard ended inside this batch)
+                    done = q_out;
                 } else {
                     p.ray.o = ld3(sc.cam_o);
                     p.ray.d = mk(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]));
@@ -1939,18 +1990,16 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         } else if (regen) {
             const uint32_t n = (uint32_t)__popcll(need);
             const uint32_t left = pool_end - pool;
-            uint32_t base = pool_end;
-            if (left < n) {
-                uint32_t b0 = 0;
+            uint32_t base = a.n_items, e = a.n_items;  // fresh items [base, e) (none once q_out)
+            if (left < n && !q_out) {
                 const uint32_t first = (uint32_t)__ffsll((unsigned long long)need) - 1u;
-                if (lane == first) b0 = atomicAdd(a.queue, grab);
-                base = __builtin_amdgcn_readfirstlane(__shfl(b0, first));
+                qgrab(a, grab, first, qk, q_seen, q_out, &base, &e);
             }
             if (!have && !done) {
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint32_t item = r < left ? pool + r : base + (r - left);
-                if (item < a.n_items) {
+                if (item < (r < left ? pool_end : e)) {
                     uint32_t j, o;
                     split_item(a, item, &j, &o);
                     int x, y;
@@ -1974,13 +2023,15 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                     slot = j * a.n_pix + o;
                     have = true;
                 } else {
-                    done = true;
+                    done = q_out;  // else the last shard ended short of this lane: next regen
                 }
             }
             if (left < n) {
-                pool = base + (n - left);
-                pool_end = base + grab;
-                grab = grab_size<GEN>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+                // a successful grab starts inside its shard, whose end is a multiple of 64
+                // beyond it: it covers the n - left <= 64 lanes that asked
+                pool = base + (n - left) < e ? base + (n - left) : e;
+                pool_end = base + grab < e ? base + grab : e;
+                grab = grab_size<GEN>(e - pool_end, shard_waves);
             } else {
                 pool += n;
             }
