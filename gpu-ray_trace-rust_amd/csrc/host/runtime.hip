@@ -122,6 +122,7 @@ struct rt_ctx {
     uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
     uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_SMALL_LAUNCH_ITEMS: launches this size or less are small
     uint32_t grid_div = 1;        // small launches behind a busy pipeline: 1/grid_div of the resident grid
+    uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_QUEUE_SHARDS)
     float last_ms = 0.f;
     std::string err;
 };
@@ -251,6 +252,18 @@ static bool pack_texels_u8(const rt_scene_desc* scene, const std::vector<DevTex>
     }
     for (auto& th : pool) th.join();
     return ok.load();
+}
+
+// Item counters of a queue launch (trace.hip qgrab).  Each grab is one device-scope atomic; on a
+// single counter they serialise once items are cheap: triangles.yml (6 primitives, kd depth 0,
+// ~24 us per item and lane) at 10 spp made 112 K of them per 1.4 ms launch, and 8 counters (one
+// shard of the items per XCD) ran it 4,937 -> 14,120 Msamples/s.  Large scenes lose with shards
+// (spaceship_r1 4096^2 -5.4%, biplane -8%, walled -0.6%: one counter keeps the whole chip on
+// one window of consecutive items), so only scenes of at most 64 primitives with triangles are
+// sharded (the sphere-only kernel's grabs are already 256 items: RT_QMIN_SPH).
+static uint32_t queue_shards(uint32_t n_spheres, uint32_t n_free_tris, size_t n_mesh_tris) {
+    const uint64_t n = (uint64_t)n_spheres + n_free_tris + n_mesh_tris;
+    return (n_free_tris + n_mesh_tris) > 0 && n <= 64 ? 8u : 1u;
 }
 
 // A pipeline slot's stream, fold event and item counter, created on the slot's first use: HIP
@@ -522,6 +535,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const size_t n_mesh = mf.tris.size();
         if ((uint64_t)scene->n_spheres + scene->n_free_tris + n_mesh >= (1ull << 30))
             return set_err(c, RT_ERR_INVALID_ARG, "too many primitives");
+        c->queue_shards = queue_shards(scene->n_spheres, scene->n_free_tris, n_mesh);
         std::vector<float4> pool(3 * ((size_t)scene->n_spheres + scene->n_free_tris + n_mesh), make_float4(0.f, 0.f, 0.f, 0.f));
         for (uint32_t i = 0; i < scene->n_spheres; ++i) pool[3 * (size_t)i] = sph[i];
         std::memcpy(pool.data() + 3 * (size_t)scene->n_spheres, ftri.data(), ftri.size() * sizeof(float4));
@@ -692,6 +706,10 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
         c->small_slots = slots_for_queues(hwq);
         c->grid_div = small_grid_div(c->small_slots);
+    }
+    if (const char* e = std::getenv("RT_QUEUE_SHARDS")) {
+        const unsigned long v = std::strtoul(e, nullptr, 10);
+        if (v >= 1 && v <= 32) c->queue_shards = (uint32_t)v;
     }
     if (const char* e = std::getenv("RT_SMALL_LAUNCH_ITEMS")) c->small_items = std::strtoull(e, nullptr, 10);
     if (const char* e = std::getenv("RT_QUEUE_GRID_DIV")) {
@@ -964,6 +982,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         if (st) return st;
         a.radiance = sl.radiance;
         a.queue = sl.queue;
+        a.n_shards = c->queue_shards;
         a.gstack = nullptr;
         if (const size_t gb = queue_gstack_bytes(a, (uint32_t)(lanes / BLOCK))) {
             if (gb > sl.gstack_cap) {

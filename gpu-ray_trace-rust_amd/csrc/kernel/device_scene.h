@@ -166,9 +166,10 @@ struct LaunchArgs {
     float* radiance;
     // Queue schedule (launch_trace_queue): persistent lanes take (pixel, sample) items
     // item = j * n_pix + o (sample j of the launch, output pixel o) in wave-sized grabs from the
-    // counters of its shards (queue[k * 32], k < RT_QSHARDS: one 128-B line each, zeroed before
-    // the launch), trace them into `radiance` and fold_kernel folds them in sample order.
+    // counters of its n_shards shards (queue[k * 32], one 128-B line each, zeroed before the
+    // launch), trace them into `radiance` and fold_kernel folds them in sample order.
     uint32_t* queue;
+    uint32_t n_shards;      // 1..32 (runtime.hip queue_shards)
     uint32_t n_items;       // n_pix * sample_count
     // Sphere-only queue kernel: its traversal stack in global memory, [block][stack_depth][BLOCK]
     // (queue_gstack_bytes), so the workgroup's LDS holds only the sphere and material tables.

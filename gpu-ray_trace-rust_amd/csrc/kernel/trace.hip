@@ -1811,24 +1811,22 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
     return g < qmin ? qmin : (g > (uint32_t)RT_QMAX ? (uint32_t)RT_QMAX : g);
 }
 
-// The launch's items in RT_QSHARDS sub-ranges, each with its own counter (a 128-B line of
-// a.queue): every grab is one device-scope atomic, and on one counter they serialise — a cheap
-// scene's 64-item grabs (triangles.yml at 10 spp: ~112 K atomics per 1.4 ms launch) waited on it
-// for most of the launch.  A wave starts on shard blockIdx % RT_QSHARDS (blocks are dealt to the
-// 8 XCDs round-robin, so each XCD starts on its own shard) and moves to the next shard when its
-// own is exhausted; it is done when it has found every shard exhausted (counters only grow).
-// Shard boundaries are multiples of 64, so a grab (a multiple of 64, at least 64) that starts
-// inside a shard covers every lane that asks.  Which lane traces an item changes, never what
-// the item computes: bit-identical images.
-#ifndef RT_QSHARDS
-#define RT_QSHARDS 8
-#endif
+// The launch's items in a.n_shards sub-ranges (1..32), each with its own counter (a 128-B line
+// of a.queue): every grab is one device-scope atomic, and on one counter they serialise — a
+// cheap scene's 64-item grabs (triangles.yml at 10 spp: ~112 K atomics per 1.4 ms launch) waited
+// on it for most of the launch.  A wave starts on shard blockIdx % n_shards (blocks are dealt to
+// the 8 XCDs round-robin, so with 8 shards each XCD starts on its own) and moves to the next
+// shard when its own is exhausted; it is done when it has found every shard exhausted (counters
+// only grow).  Shard boundaries are multiples of 64, so a grab (a multiple of 64, at least 64)
+// that starts inside a shard covers every lane that asks.  Which lane traces an item changes,
+// never what the item computes: bit-identical images.  The runtime shards only small scenes
+// (runtime.hip queue_shards): on the mesh scenes one counter, whose waves all work on one
+// window of consecutive items, ran 5-8% faster than 8 shards.
 constexpr uint32_t QSHARD_STRIDE = 32;  // uint32 words between shard counters (128 B)
-static_assert(RT_QSHARDS >= 1 && RT_QSHARDS <= 32, "RT_QSHARDS: 1..32 (a.queue holds 32 lines)");
-__device__ __forceinline__ uint32_t qshard_begin(uint32_t n_items, uint32_t k) {
+__device__ __forceinline__ uint32_t qshard_begin(const LaunchArgs& a, uint32_t k) {
     if (k == 0) return 0u;
-    const uint64_t b = ((uint64_t)n_items * k / RT_QSHARDS + 63u) & ~63ull;
-    return b < n_items ? (uint32_t)b : n_items;
+    const uint64_t b = ((uint64_t)a.n_items * k / a.n_shards + 63u) & ~63ull;
+    return b < a.n_items ? (uint32_t)b : a.n_items;
 }
 // One grab of `grab` items for the wave (wave-uniform; `lane_op` is the lane that issues the
 // atomic): from shard qk, moving on while shards are exhausted.  Returns [*base, *end) (end the
@@ -1837,7 +1835,7 @@ __device__ __forceinline__ void qgrab(const LaunchArgs& a, uint32_t grab, uint32
                                       uint32_t& q_seen, bool& exhausted, uint32_t* base, uint32_t* end) {
     const uint32_t lane = __lane_id();
     for (;;) {
-        const uint32_t b = qshard_begin(a.n_items, qk), e = qshard_begin(a.n_items, qk + 1);
+        const uint32_t b = qshard_begin(a, qk), e = qshard_begin(a, qk + 1);
         uint32_t b0 = 0;
         if (lane == lane_op) b0 = atomicAdd(a.queue + qk * QSHARD_STRIDE, grab);
         const uint32_t off = __builtin_amdgcn_readfirstlane(__shfl(b0, lane_op));
@@ -1846,12 +1844,12 @@ __device__ __forceinline__ void qgrab(const LaunchArgs& a, uint32_t grab, uint32
             *end = e;
             return;
         }
-        if (++q_seen >= RT_QSHARDS) {  // every shard exhausted: no items
+        if (++q_seen >= a.n_shards) {  // every shard exhausted: no items
             exhausted = true;
             *base = *end = a.n_items;
             return;
         }
-        qk = qk + 1 == RT_QSHARDS ? 0u : qk + 1;
+        qk = qk + 1 == a.n_shards ? 0u : qk + 1;
     }
 }
 
@@ -1912,10 +1910,10 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint32_t grab = grab_size<GEN>(a.n_items / RT_QSHARDS, (n_waves + RT_QSHARDS - 1) / RT_QSHARDS);
-    uint32_t qk = blockIdx.x % RT_QSHARDS, q_seen = 0;  // wave-uniform: its shard, shards found exhausted
+    const uint32_t shard_waves = (n_waves + a.n_shards - 1) / a.n_shards;
+    uint32_t grab = grab_size<GEN>(a.n_items / a.n_shards, shard_waves);
+    uint32_t qk = blockIdx.x % a.n_shards, q_seen = 0;  // wave-uniform: its shard, shards found exhausted
     bool q_out = false;                                 // wave-uniform: every shard exhausted
-    const uint32_t shard_waves = (n_waves + RT_QSHARDS - 1) / RT_QSHARDS;
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
