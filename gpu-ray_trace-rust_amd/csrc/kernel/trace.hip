@@ -1910,8 +1910,10 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    const bool batch_ok = !GEN && !sc.has_lens && a.pix_q != nullptr;
     const uint32_t shard_waves = (n_waves + a.n_shards - 1) / a.n_shards;
-    uint32_t grab = grab_size<GEN>(a.n_items / a.n_shards, shard_waves);
+    // (the batch starts use one counter over all the items: the first grab is sized for that)
+    uint32_t grab = batch_ok ? grab_size<GEN>(a.n_items, n_waves) : grab_size<GEN>(a.n_items / a.n_shards, shard_waves);
     uint32_t qk = blockIdx.x % a.n_shards, q_seen = 0;  // wave-uniform: its shard, shards found exhausted
     bool q_out = false;                                 // wave-uniform: every shard exhausted
     bool have = false, done = false;
@@ -1919,7 +1921,6 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     Path p;
     // RT_START_BATCH: the wave's current batch of starts, entries [st_pos, 64) not yet taken
     uint32_t st_pos = 64u, st_n = 0u;
-    const bool batch_ok = !GEN && !sc.has_lens && a.pix_q != nullptr;
 #if RT_TIMING
     // sphere-only kernel: wave clock in path starts, normalize, closest hit and shading
     unsigned long long tq_regen = 0, tq_norm = 0, tq_closest = 0, tq_shade = 0, tq_seg = 0;
@@ -1948,18 +1949,19 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             };
             if (idle && r < st_n) take(st_pos + r);  // before the next batch overwrites them
             if (n > st_n) {
-                if (pool >= pool_end) {  // grabs and shards are multiples of 64: a batch spans neither
-                    uint32_t qe = a.n_items;  // (but the last shard may end inside its last batch)
-                    pool = pool_end = a.n_items;  // past the items: START_NONE entries
-                    if (!q_out) {
-                        qgrab(a, grab, 0u, qk, q_seen, q_out, &pool, &qe);
-                        pool_end = pool + grab < qe ? pool + grab : qe;
-                        grab = grab_size<GEN>(qe - pool_end, shard_waves);
-                    }
+                // One counter (a.queue[0] over all the items, whatever a.n_shards): the sphere-only
+                // kernel's grabs are 256+ items (RT_QMIN_SPH), and the shard walk of qgrab cost
+                // walled 1.7% here.
+                if (pool == pool_end) {  // grabs are multiples of 64: a batch never spans two
+                    uint32_t b0 = 0;
+                    if (lane == 0) b0 = atomicAdd(a.queue, grab);
+                    pool = __builtin_amdgcn_readfirstlane(b0);
+                    pool_end = pool + grab;
+                    grab = grab_size<GEN>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
                 }
                 __builtin_amdgcn_wave_barrier();
-                make_start(a, sc, pool < pool_end ? pool + lane : a.n_items, lane, e);
-                if (pool < pool_end) pool += 64u;
+                make_start(a, sc, pool + lane, lane, e);
+                pool += 64u;
                 __builtin_amdgcn_wave_barrier();
                 if (idle && r >= st_n) take(r - st_n);
                 st_pos = n - st_n;
@@ -1969,10 +1971,8 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                 st_n -= n;
             }
             if (idle) {
-                if (v[5] == START_NONE) {
-                    // past the items: done once every shard is exhausted, else the lane takes
-                    // the next batch's entry (the last shard ended inside this batch)
-                    done = q_out;
+                if (v[5] == START_NONE) {  // past the launch's items
+                    done = true;
                 } else {
                     p.ray.o = ld3(sc.cam_o);
                     p.ray.d = mk(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]));
@@ -1988,16 +1988,24 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         } else if (regen) {
             const uint32_t n = (uint32_t)__popcll(need);
             const uint32_t left = pool_end - pool;
-            uint32_t base = a.n_items, e = a.n_items;  // fresh items [base, e) (none once q_out)
-            if (left < n && !q_out) {
+            // fresh items [base, e): the general kernel's sharded counters (none once q_out);
+            // the sphere-only kernel keeps one counter (its lens cameras start here)
+            uint32_t base = a.n_items, e = a.n_items;
+            if (left < n && (!GEN || !q_out)) {
                 const uint32_t first = (uint32_t)__ffsll((unsigned long long)need) - 1u;
-                qgrab(a, grab, first, qk, q_seen, q_out, &base, &e);
+                if constexpr (GEN) {
+                    qgrab(a, grab, first, qk, q_seen, q_out, &base, &e);
+                } else {
+                    uint32_t b0 = 0;
+                    if (lane == first) b0 = atomicAdd(a.queue, grab);
+                    base = __builtin_amdgcn_readfirstlane(__shfl(b0, first));
+                }
             }
             if (!have && !done) {
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint32_t item = r < left ? pool + r : base + (r - left);
-                if (item < (r < left ? pool_end : e)) {
+                if (GEN ? item < (r < left ? pool_end : e) : item < a.n_items) {
                     uint32_t j, o;
                     split_item(a, item, &j, &o);
                     int x, y;
@@ -2021,15 +2029,21 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                     slot = j * a.n_pix + o;
                     have = true;
                 } else {
-                    done = q_out;  // else the last shard ended short of this lane: next regen
+                    done = !GEN || q_out;  // else the last shard ended short of this lane: next regen
                 }
             }
             if (left < n) {
-                // a successful grab starts inside its shard, whose end is a multiple of 64
-                // beyond it: it covers the n - left <= 64 lanes that asked
-                pool = base + (n - left) < e ? base + (n - left) : e;
-                pool_end = base + grab < e ? base + grab : e;
-                grab = grab_size<GEN>(e - pool_end, shard_waves);
+                if constexpr (GEN) {
+                    // a successful grab starts inside its shard, whose end is a multiple of 64
+                    // beyond it: it covers the n - left <= 64 lanes that asked
+                    pool = base + (n - left) < e ? base + (n - left) : e;
+                    pool_end = base + grab < e ? base + grab : e;
+                    grab = grab_size<GEN>(e - pool_end, shard_waves);
+                } else {
+                    pool = base + (n - left);
+                    pool_end = base + grab;
+                    grab = grab_size<GEN>(a.n_items > pool_end ? a.n_items - pool_end : 0u, n_waves);
+                }
             } else {
                 pool += n;
             }

@@ -10,7 +10,7 @@ mkdir -p lib/variants build/variants
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-rdc -munsafe-fp-atomics"
 for spec in "$@"; do
   name=${spec%%=*}; defs=${spec#*=}
-  hipcc $FLAGS -fno-slp-vectorize $defs -c -o build/variants/trace_$name.o csrc/kernel/trace.hip &
+  hipcc $FLAGS -fno-slp-vectorize $defs -c -o build/variants/trace_$name.o csrc/kernel/${SRC:-trace.hip} &
   hipcc $FLAGS $defs -c -o build/variants/runtime_$name.o csrc/host/runtime.hip &
   wait
   hipcc --offload-arch=gfx950 -shared -o lib/variants/librt_$name.so build/kd_build.o build/mesh_flatten.o build/doc.o build/pack.o build/scheme_host.o build/variants/runtime_$name.o build/variants/trace_$name.o -lz
