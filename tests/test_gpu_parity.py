@@ -476,6 +476,55 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
         assert np.array_equal(full, o_full), (cfg, parity.stats(full, o_full))
 
 
+@pytest.mark.parametrize("scene_name,spp", [("triangles", 4), ("biplane", 2), ("walled", 6)])
+def test_queue_shards_bit_invariant(gpu_available, oracle, monkeypatch, scene_name, spp):
+    """The queue's items in 1, 3, 8 or 32 shards with a counter each (trace.hip qgrab: a wave
+    starts on its own shard and walks on when it is exhausted; the last shard may end inside a
+    grab) render the forward oracle's image bit for bit, on a frame whose item count is not a
+    multiple of 64 and on tiles; the sphere-only kernel ignores the shards (one counter)."""
+    from rt_amd import render
+
+    sc = load_scene(scene_name, width=203, height=97)  # 19,691 pixels: shards end off the 64 grid
+    w, h = sc.info.width, sc.info.height
+    tiles = [(w // 2 - 40, h // 2 - 20, 80, 40), (0, h - 7, 33, 7)]
+    o_full = oracle.render(sc, [(0, 0, w, h)], 0, spp, accum=oracle.ACCUM_FORWARD)
+    o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
+    for n in ("1", "3", "8", "32"):
+        monkeypatch.setenv("RT_QUEUE_SHARDS", n)
+        with render.Context(sc) as c:
+            full = c.render(None, 0, spp)
+            got = c.render(tiles, 0, spp)
+        assert np.array_equal(full, o_full), (n, parity.stats(full, o_full))
+        assert np.array_equal(got, o_tiles), (n, parity.stats(got, o_tiles))
+
+
+def test_small_launch_pipeline_bit_invariant(gpu_available, oracle, monkeypatch):
+    """Small overlapped launches (a380's batch of 1 spp): 12 pipeline slots, each launch behind a
+    busy pipeline on 1/8 of the resident grid (runtime.hip slots_for_queues / small_grid_div),
+    async calls back to back, equal the oracle over the same samples bit for bit — also with 1/2
+    and 1/16 of the grid and 3 slots."""
+    import torch
+
+    from rt_amd import render
+
+    sc = load_scene("a380", width=160, height=80)
+    w, h = sc.info.width, sc.info.height
+    spp = 6
+    o = oracle.render(sc, [(0, 0, w, h)], 0, spp, accum=oracle.ACCUM_FORWARD)
+    for slots, div in (("12", "8"), ("12", "2"), ("3", "16")):
+        monkeypatch.setenv("RT_PIPELINE_SLOTS", slots)
+        monkeypatch.setenv("RT_QUEUE_GRID_DIV", div)
+        with render.Context(sc) as c:
+            out = torch.zeros((w * h, 4), dtype=torch.float32, device="cuda:0")
+            stream = torch.cuda.current_stream().cuda_stream
+            for s0 in range(spp):  # one sample per call: every launch is small
+                c.render_device_async(out.data_ptr(), [(0, 0, w, h)], s0, 1, stream=stream)
+            c.synchronize()
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().reshape(h, w, 4)
+        assert np.array_equal(got, o.reshape(h, w, 4)), (slots, div, parity.stats(got, o.reshape(h, w, 4)))
+
+
 def test_sphere_scene_with_lens_bit_exact(gpu_available, oracle):
     """walled.yml with its commented-out lens (`lens_r: 0.1`): the sphere-only kernel keeps the
     per-lane path starts for lens cameras (RT_START_BATCH covers lens-free ones), and both render
