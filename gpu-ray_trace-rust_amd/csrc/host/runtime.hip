@@ -968,6 +968,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         const bool small = a.n_items <= c->small_items;
         // a small launch behind a launch still running takes a share of the grid (see N_SLOTS)
         const bool busy = c->last_fold && hipEventQuery(c->last_fold) == hipErrorNotReady;
+        (void)hipGetLastError();  // a not-ready query is no error for the launch checks below
         const uint32_t n_slots = c->n_slots ? c->n_slots : (small ? c->small_slots : 2u);
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
         for (uint32_t k = 0; k < (overlap ? n_slots : 1u); ++k) {
