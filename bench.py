@@ -4,8 +4,13 @@
 One step = one batch (the reference's gpu_render_batch, walled.yml: 1000 spp) over this rank's
 pixels: rt_render_device_async, which overlaps step i + 1's trace with step i's drain tail
 (draw_scene.rs:30-44's batches are independent sample ranges; only their running-mean folds are
-ordered), plus — for N > 1 — the frame-end RCCL gather of every rank's tile radiance to rank 0,
-on torch's stream behind the step's fold (rt_amd/shard.py FrameSteps).  Inputs (scene, KD tree)
+ordered).  For N > 1 the ranks' tile radiance is gathered to rank 0 by RCCL on torch's stream
+behind the last step's fold, once per frame (`--gather frame`, north_star's single frame-end
+gather; the default), or after every step (`--gather step`, the reference's per-batch
+read-back); the line reports the other mode beside the headline (rt_amd/shard.py FrameSteps).
+`value_host_inclusive` adds one D2H copy of the final frame to the timed steps (SURVEY.md §8d:
+"to final result on host"); `value` is the device-resident rate.  `bench_schema` 4: `value` is
+strong scaling (since round 3) and `weak` always holds the weak-scaling figure (N = 1: the same).  Inputs (scene, KD tree)
 are resident in HBM before the timed region.  N GPUs: one process per GPU
 (torch.distributed.run), image rows dealt to ranks as stripes of up to 8 rows, round-robin
 (rt_amd.shard.stripe_rows).
@@ -31,8 +36,10 @@ on the host's cores at BASELINE.md §2's sample counts.
 
 At N = 1 the line also carries `configs`: BASELINE.json's other single-GPU configs, each timed by
 this run — a380 (10 spp in batches of 1), biplane (200 spp in batches of 10), spaceship_r1 at
-4096^2 (25-spp steps: one GPU's share of config 5), and triangles (config 0, 10 spp) — each with
-its own roofline and CPU baseline.
+4096^2 (25-spp steps: one GPU's share of config 5), and triangles (config 0, 10 spp) — each run as
+render_to_target_gpu's batch loop on the device (rt_render_batches_device_async: every batch's
+frame, consecutive small batches traced by one launch), with its own roofline and CPU baseline;
+a380 also in a child process at HIP's default of 4 hardware queues (`hw_queues_4`).
 """
 from __future__ import annotations
 
@@ -54,7 +61,7 @@ try:
     _q = int(HW_QUEUES_BEFORE or "0")
 except ValueError:
     _q = 0
-if _q < 16:
+if _q < 16 and "--config-only" not in sys.argv:  # config_at_queues' child keeps the value it was given
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import rt_amd  # noqa: E402
 
@@ -67,6 +74,8 @@ VALU_PEAK_WINST_S = 256 * 4 * 2.4e9 / 2
 BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits": 32, "mesh_hits": 132}
 # the CPU baseline's sample count per scene (steady-state per-sample throughput)
 CPU_SPP = {"walled": 20, "biplane": 10, "a380": 2, "spaceship_r1@4096": 1, "spaceship_r1": 2, "triangles": 10}
+# ... over every k-th row only where a full frame takes more than ~10 s of CPU per call
+CPU_ROWS_STEP = {"spaceship_r1@4096": 4}
 # BASELINE.json configs timed beside the headline at N = 1: name -> (scene, total spp, batch,
 # width, height, timed repetitions of the whole config, warmup repetitions)
 CONFIGS = {
@@ -205,12 +214,18 @@ def cgroup_cpus():
         return None
 
 
-def cpu_baseline(loaded, spp, threads=None):
+def cpu_baseline(loaded, spp, threads=None, reps=3, rows_step=1):
     """The oracle (C++ restatement of render_to_target_cpu, recursive radiance) over the full
     frame at `spp` samples per pixel, one thread per CPU the process may use
     (the reference's rayon par_iter_mut uses all of them, draw_scene.rs:73).  The KD build and
-    scene setup are timed apart (an oracle call with 0 samples), as SURVEY.md §8d asks.  `cores`
-    is the CPU time actually available: the thread count capped by the cgroup's CPU quota."""
+    scene setup are timed apart (an oracle call with 0 samples), as SURVEY.md §8d asks.
+    `reps` timed repetitions: the median is `value`, with the min / max beside it, and the
+    process CPU time over each call (os.times: every thread of this process) gives the CPU the
+    threads actually got — `effective_cores` = CPU-seconds / wall-seconds — and a per-core rate.
+    rows_step > 1 renders every rows_step-th row only (one-row tiles over the whole frame: the
+    same mix of pixels, a bounded sample of a frame too large for a few seconds of CPU)."""
+    import statistics
+
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py  # test infrastructure: the CPU baseline leg only
 
@@ -220,16 +235,26 @@ def cpu_baseline(loaded, spp, threads=None):
     # quota (256 threads under a 16-CPU quota only contend for the same 16 CPUs' time)
     threads = threads or max(1, min(affinity, int(quota + 0.5) if quota else affinity))
     w, h = int(loaded.info.width), int(loaded.info.height)
-    full = [(0, 0, w, h)]
+    tiles = [(0, 0, w, h)] if rows_step <= 1 else [(0, y, w, 1) for y in range(0, h, rows_step)]
+    npix = sum(t[2] * t[3] for t in tiles)
 
     def timed(n):
-        t0 = time.perf_counter()
-        oracle_py.render(loaded, full, 0, n, threads=threads)
-        return time.perf_counter() - t0
+        c0, t0 = os.times(), time.perf_counter()
+        oracle_py.render(loaded, tiles, 0, n, threads=threads)
+        t1, c1 = time.perf_counter(), os.times()
+        return t1 - t0, (c1.user - c0.user) + (c1.system - c0.system)
 
     timed(0)  # one-time loading
-    t_build = min(timed(0), timed(0))
-    dt = timed(spp) - t_build
+    t_build = min(timed(0)[0], timed(0)[0])
+    runs = []
+    for _ in range(reps):
+        wall, cpu = timed(spp)
+        dt = wall - t_build
+        runs.append({"Msamples_s": npix * spp / dt / 1e6, "wall_s": wall, "cpu_s": cpu,
+                     "effective_cores": cpu / wall})
+    vals = sorted(r["Msamples_s"] for r in runs)
+    med = statistics.median(vals)
+    eff = statistics.median(r["effective_cores"] for r in runs)
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -239,12 +264,17 @@ def cpu_baseline(loaded, spp, threads=None):
     except OSError:
         pass
     cores = min(threads, quota) if quota else threads
-    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+    what = f"full {w}x{h} frame" if rows_step <= 1 else f"every {rows_step}th row of the {w}x{h} frame ({npix} pixels)"
+    return {"value": round(med, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "reps": reps, "min": round(vals[0], 4), "max": round(vals[-1], 4),
+            "spread": round((vals[-1] - vals[0]) / med, 4),
+            "effective_cores": round(eff, 2), "value_per_effective_core": round(med / eff, 4),
+            "runs": [{k: round(v, 3) for k, v in r.items()} for r in runs],
             "threads": threads, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "cpu_model": model,
             "kd_build_s": round(t_build, 3),
-            "sample": f"full {w}x{h} frame, {spp} spp (BASELINE.md §2) in one call on {threads} threads "
-                      f"({dt:.1f} s after the KD build, CPU quota {quota or 'none'}); oracle/oracle.cpp "
-                      f"recursive radiance"}
+            "sample": f"{what}, {spp} spp (BASELINE.md §2), {reps} calls on {threads} threads, median "
+                      f"(KD build timed apart, CPU quota {quota or 'none'}); oracle/oracle.cpp recursive radiance; "
+                      f"effective_cores = process CPU-seconds / wall-seconds of each call"}
 
 
 def kernel_label(loaded):
@@ -252,8 +282,8 @@ def kernel_label(loaded):
     spheres_only = (loaded.desc.n_free_tris == 0 and loaded.desc.n_meshes == 0
                     and loaded.desc.n_spheres <= 64 and not int(loaded.info.dir_light_samp))
     dls = int(loaded.info.dir_light_samp) != 0
-    restart = spheres_only or os.environ.get("RT_KD_RESTART", "0") not in ("0", "")
-    slab = os.environ.get("RT_KD_RESTART") == "2"
+    restart = spheres_only or os.environ.get("RT_DEBUG_KD_RESTART", "0") not in ("0", "")
+    slab = os.environ.get("RT_DEBUG_KD_RESTART") == "2"
     b = lambda v: "true" if v else "false"  # noqa: E731
     return f"rtd::queue_kernel<{b(not spheres_only)}, {b(dls)}, {b(restart)}, {b(slab)}>"
 
@@ -273,10 +303,18 @@ def sync_kernel_ms(ctx, tiles, sample, spp):
     return ls["trace_ms"] / max(ls["n_timed_launches"], 1)
 
 
-def run_config(name, cpu, build_id):
+GROUP_ITEMS = 1 << 24  # rt_render_to_target's batch groups (runtime.hip GROUP_ITEMS)
+
+
+def run_config(name, cpu, build_id, per_batch_calls=True):
     """One BASELINE.json config on this GPU: the whole config (its total spp in the scheme's
-    batches, async, pipelined) `reps` times after `warm` untimed runs; Msamples/s over the timed
-    runs, the roofline of its trace launches and the CPU baseline at BASELINE.md §2's spp."""
+    batches) `reps` times after `warm` untimed runs, the way render_to_target_gpu's batch loop runs
+    on the device (rt_render_batches_device_async: batch k's frame into its own buffer, consecutive
+    batches traced together in groups of up to GROUP_ITEMS samples, as rt_render_to_target groups
+    them).  Beside it: the same config as one async call per batch (rt_render_device_async, the
+    round-3 method, which needs a hardware queue per batch in flight), and the host-inclusive rate
+    (the last frame copied to host memory inside the timed region).  Then the roofline of its
+    trace launches and the CPU baseline at BASELINE.md §2's spp."""
     import torch
 
     from rt_amd import render
@@ -285,44 +323,82 @@ def run_config(name, cpu, build_id):
     _, loaded = load(scene, width, height)
     w, h = int(loaded.info.width), int(loaded.info.height)
     tiles = [(0, 0, w, h)]
-    res = {"workload": f"{scene}.yml {w}x{h}, {total} spp in batches of {batch} "
-                       f"({total // batch} async calls), kd_tree_depth {int(loaded.info.kd_tree_depth)}"}
+    nb = total // batch
+    group = max(1, min(nb, GROUP_ITEMS // (w * h * batch)))
+    res = {"workload": f"{scene}.yml {w}x{h}, {total} spp in batches of {batch}, kd_tree_depth "
+                       f"{int(loaded.info.kd_tree_depth)}; {nb} batches per run, each batch's frame in its own "
+                       f"device buffer, traced {group} batches per launch"}
     with render.Context(loaded) as ctx:
-        out = torch.zeros((w * h, 4), dtype=torch.float32, device="cuda:0")
+        outs = [torch.zeros((w * h, 4), dtype=torch.float32, device="cuda:0") for _ in range(nb)]
         stream = torch.cuda.current_stream().cuda_stream
         sample = 0
 
-        def whole():
+        def whole_batches():
             nonlocal sample
-            for _ in range(total // batch):
-                ctx.render_device_async(out.data_ptr(), tiles, sample, batch, stream=stream)
+            for g0 in range(0, nb, group):
+                ptrs = [o.data_ptr() for o in outs[g0:g0 + group]]
+                ctx.render_batches_device_async(ptrs, tiles, sample, batch, stream=stream)
+                sample += batch * len(ptrs)
+
+        def whole_calls():
+            nonlocal sample
+            for k in range(nb):
+                ctx.render_device_async(outs[k].data_ptr(), tiles, sample, batch, stream=stream)
                 sample += batch
 
-        for _ in range(warm):
-            whole()
-        ctx.synchronize()
-        torch.cuda.synchronize()
+        def timed(fn):
+            for _ in range(warm):
+                fn()
+            ctx.synchronize()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            ctx.synchronize()
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0, ctx.launch_stats()
+
+        elapsed, ls = timed(whole_batches)
+        # the final result on the host: the last frame's D2H copy, timed after the run
         t0 = time.perf_counter()
-        for _ in range(reps):
-            whole()
-        ctx.synchronize()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        ls = ctx.launch_stats()
-        kms = sync_kernel_ms(ctx, tiles, sample, batch)
-        ok = bool((out[:, 3] == 1.0).all().item())
-    per_launch = w * h * batch
-    res.update(value=round(w * h * total * reps / elapsed / 1e6, 3), unit="Msamples/s", spp=total, batch=batch,
-               reps=reps, elapsed_s=round(elapsed, 4), frame_complete=ok,
+        last = outs[nb - 1].cpu()
+        elapsed_host = elapsed + time.perf_counter() - t0
+        del last
+        # one call per batch only differs when batches are grouped
+        per_calls = timed(whole_calls)[0] if per_batch_calls and group > 1 else None
+        per_launch = w * h * batch * group
+        kms = sync_kernel_ms(ctx, tiles, sample, batch * group)
+        ok = bool((outs[nb - 1][:, 3] == 1.0).all().item())
+    rate = lambda t: round(w * h * total * reps / t / 1e6, 3)  # noqa: E731
+    res.update(value=rate(elapsed), unit="Msamples/s", spp=total, batch=batch, batches_per_launch=group, reps=reps,
+               elapsed_s=round(elapsed, 4), frame_complete=ok, value_host_inclusive=rate(elapsed_host),
                launch={"trace_launches": ls["n_trace_launches"], "samples_per_launch": per_launch,
                        "trace_ms_per_launch_overlapped": round(ls["trace_ms"] / max(ls["n_timed_launches"], 1), 3),
                        "trace_ms_per_launch_sync": round(kms, 3)})
+    if per_calls is not None:
+        res["value_per_batch_calls"] = rate(per_calls)
     res["roofline"] = roofline(scene if name != "spaceship_r1@4096" else "spaceship_r1", per_launch, kms, build_id,
                                kernel_label(loaded), "one synchronous launch (no overlap)")
     if cpu:
-        res["cpu_baseline"] = cpu_baseline(loaded, CPU_SPP[name])
+        res["cpu_baseline"] = cpu_baseline(loaded, CPU_SPP[name], rows_step=CPU_ROWS_STEP.get(name, 1))
         res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     return res
+
+
+def config_at_queues(name, queues):
+    """run_config in a child process that starts HIP with GPU_MAX_HW_QUEUES = `queues` (HIP reads
+    it once, at start): what a caller who leaves HIP's default of 4 gets.  The child is started
+    with subprocess (fork + exec before it touches the GPU), never by replacing this process."""
+    import subprocess
+
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(queues))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config-only", name], env=env,
+                       capture_output=True, text=True, timeout=600)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode or not line:
+        return {"error": (r.stderr or r.stdout)[-500:]}
+    d = json.loads(line[-1])
+    return {k: d[k] for k in ("value", "value_per_batch_calls", "hw_queues") if k in d}
 
 
 def main():
@@ -351,7 +427,18 @@ def main():
                     help="gloo: gather host copies (multi-rank test with every rank on one GPU)")
     ap.add_argument("--same-device", action="store_true", help="every rank on device 0 (tests; gloo only)")
     ap.add_argument("--dump-frame", default=None, help="rank 0 saves the last assembled frame (.npy)")
+    ap.add_argument("--gather", default="frame", choices=("frame", "step"),
+                    help="N > 1: gather the ranks' tiles once at frame end (north_star; default) or after every "
+                         "step (the reference's per-batch read-back); the other mode is reported beside it")
+    ap.add_argument("--config-only", default=None, choices=sorted(CONFIGS),
+                    help="print one BASELINE config's JSON (no CPU leg) and exit: bench's child for the "
+                         "4-queue a380 figure")
     args = ap.parse_args()
+    if args.config_only:
+        r = run_config(args.config_only, False, None)
+        r["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
+        print(json.dumps(r), flush=True)
+        return
     if args.same_device and args.dist_backend != "gloo":
         raise SystemExit("--same-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
 
@@ -388,17 +475,18 @@ def main():
 
     ctx = render.Context(loaded, device=local)
 
-    def timed_run(strong_mode):
+    def timed_run(strong_mode, gather):
         spp_rank, job_samples = step_samples(w, h, spp, shard_world, strong_mode)
         fs = FrameSteps(ctx, tiles, w, h, rank, world, stripe, spp_rank, local, dist=dist,
-                        backend=args.dist_backend, sync=args.sync)
+                        backend=args.dist_backend, sync=args.sync, gather=gather)
         r = fs.run(args.steps, args.warmup)
         if args.as_rank:
             job_samples = fs.npix * spp_rank  # one rank's share only
-        r.update(spp_rank=spp_rank, npix=fs.npix, value=job_samples * args.steps / r["elapsed_s"] / 1e6)
+        r.update(spp_rank=spp_rank, npix=fs.npix, value=job_samples * args.steps / r["elapsed_s"] / 1e6,
+                 value_host_inclusive=job_samples * args.steps / (r["elapsed_s"] + r["host_copy_s"]) / 1e6)
         return fs, r
 
-    fs, r = timed_run(strong)
+    fs, r = timed_run(strong, args.gather)
     elapsed, ls, spp_rank, npix = r["elapsed_s"], r["launch"], r["spp_rank"], r["npix"]
     # after the timed region: rank 0 reassembles the last gathered frame and checks that every
     # pixel was rendered by some rank (alpha is 1 exactly where written)
@@ -417,6 +505,7 @@ def main():
     kernel_ms = ls["trace_ms"] / max(ls.get("n_timed_launches", n_launch), 1)
     res = {"metric": f"Msamples/s (pixels x spp / s) on {args.scene}.yml",
            "value": round(r["value"], 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+           "bench_schema": 4,
            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
            "dtype": "f32",
@@ -428,21 +517,37 @@ def main():
                       "parallelism": f"tiles{world}", "dispatch": "sync" if args.sync else "async",
                       "dist_backend": args.dist_backend if world > 1 else None}}
     res["frame_complete"] = frame_complete
+    # the final frame on the host (SURVEY.md §8d "to final result on host"): one D2H copy of the
+    # (gathered) frame after the timed steps, added to their time; `value` stays device-resident
+    res["value_host_inclusive"] = round(r["value_host_inclusive"], 3)
+    res["host_copy_ms"] = round(r["host_copy_s"] * 1e3, 3)
     res["launch"] = {"trace_launches_per_step": n_launch / args.steps, "samples_per_launch": round(per_launch),
                      "trace_ms_per_launch": round(kernel_ms, 3),
                      "device_window_ms": round(ls["render_ms"], 3)}
     res["hw_queues"] = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "caller_value": HW_QUEUES_BEFORE,
                         "hip_started_before_rt_amd": rt_amd.hw_queues()["hip_started_before_import"]}
     if "gather_ms_per_step" in r:
+        res["gather"] = {"mode": r["gather_mode"], "gathers": r["gathers"],
+                         "ms_per_gather": round(r["gather_ms_per_gather"], 3)}
         res["gather_ms_per_step"] = round(r["gather_ms_per_step"], 3)
     if args.as_rank:
         res["config"]["rehearsal"] = f"rank {shard_rank} of {shard_world}, single GPU, no gather"
         res["scaling"] = None
-    if world > 1:  # weak scaling beside the strong headline (each rank keeps the 1-GPU step's work)
-        _, rw = timed_run(not strong)
+    if world > 1:
+        # the other gather mode (frame end <-> every step), same scaling as the headline
+        other = "step" if args.gather == "frame" else "frame"
+        _, rg = timed_run(strong, other)
+        res[f"gather_{other}"] = {
+            "value": round(rg["value"], 3), "ms_per_step": round(rg["elapsed_s"] / args.steps * 1e3, 3),
+            "gathers": rg["gathers"], "ms_per_gather": round(rg.get("gather_ms_per_gather", 0.0), 3),
+            "gather_ms_per_step": round(rg.get("gather_ms_per_step", 0.0), 3)}
+        # weak scaling beside the strong headline (each rank keeps the 1-GPU step's work)
+        _, rw = timed_run(not strong, args.gather)
         res["weak" if strong else "strong"] = {
             "value": round(rw["value"], 3), "ms_per_step": round(rw["elapsed_s"] / args.steps * 1e3, 3),
             "spp_per_rank_step": rw["spp_rank"], "gather_ms_per_step": round(rw.get("gather_ms_per_step", 0.0), 3)}
+    elif not args.as_rank:
+        res["weak"] = {"value": res["value"], "note": "N = 1: weak and strong scaling are the same run"}
 
     build_id = abi.kernel_build_id()
     if rank == 0 and not args.no_roofline:
@@ -470,6 +575,8 @@ def main():
         res["configs"] = {}
         for name in CONFIGS:
             res["configs"][name] = run_config(name, not args.no_cpu, build_id)
+        # config 2 as a caller that leaves HIP's default of 4 hardware queues gets it
+        res["configs"]["a380"]["hw_queues_4"] = config_at_queues("a380", 4)
     if dist:
         dist.destroy_process_group()
     if rank == 0:

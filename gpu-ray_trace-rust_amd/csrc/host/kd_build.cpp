@@ -170,9 +170,22 @@ struct Frontier {
 // depth `stop` (when frontier != nullptr) are not expanded: they become frontier nodes, built
 // later as subtrees of their own.  The node order within the subtree is the breadth-first order
 // of the whole build restricted to it, so merging (merge_bfs) reproduces the sequential numbering.
-static void build_subtree(const std::vector<Renderable>& rs, const std::vector<float>& cen, std::vector<uint32_t> elems,
-                          uint32_t depth0, uint32_t max_depth, uint32_t stop, SubTree* out,
-                          std::vector<Frontier>* frontier) {
+// Limits of the flat layout: node and ref indices fit 30 bits (rt_kd_node.b holds index << 2), and
+// a level's concatenated element lists are indexed by uint32.  `budget` counts the nodes and refs
+// of the whole build (all threads): past 2^30 of either the build stops with RT_ERR_OOM instead of
+// growing to the end (a tree whose elements straddle every split copies them at every level).
+struct BuildBudget {
+    std::atomic<uint64_t> nodes{0}, refs{0};
+    std::atomic<bool> over{false};
+    bool charge(uint64_t n, uint64_t r) {
+        if (over.load(std::memory_order_relaxed)) return false;
+        if (nodes.fetch_add(n) + n >= (1ull << 30) || refs.fetch_add(r) + r >= (1ull << 30)) over = true;
+        return !over.load(std::memory_order_relaxed);
+    }
+};
+static int build_subtree(const std::vector<Renderable>& rs, const std::vector<float>& cen, std::vector<uint32_t> elems,
+                         uint32_t depth0, uint32_t max_depth, uint32_t stop, SubTree* out,
+                         std::vector<Frontier>* frontier, BuildBudget* budget) {
     // Level by level: a level's element lists concatenated in one array (no per-node vectors),
     // its items in breadth-first order; the children of level L are level L + 1, in order.
     struct Item { uint32_t node; uint32_t begin, end; };
@@ -195,6 +208,7 @@ static void build_subtree(const std::vector<Renderable>& rs, const std::vector<f
                 nd.a = n;
                 nd.axis = RT_KD_LEAF;
                 nd.ref_off = (uint32_t)out->refs.size();
+                if (!budget->charge(0, n)) return RT_ERR_OOM;
                 out->refs.insert(out->refs.end(), cur.begin() + it.begin, cur.begin() + it.end);
                 if (depth > out->max_leaf_depth) out->max_leaf_depth = depth;
                 continue;
@@ -212,6 +226,7 @@ static void build_subtree(const std::vector<Renderable>& rs, const std::vector<f
             const uint32_t hb = (uint32_t)nxt.size();
             for (uint32_t k = it.begin; k < it.end; ++k)
                 if (rs[cur[k]].hi[axis] >= split) nxt.push_back(cur[k]);
+            if (nxt.size() >= (1ull << 32) || !budget->charge(2, 0)) return RT_ERR_OOM;
             nitems.push_back(Item{child, lb, hb});
             nitems.push_back(Item{child + 1, hb, (uint32_t)nxt.size()});
             out->nodes.emplace_back();
@@ -220,6 +235,7 @@ static void build_subtree(const std::vector<Renderable>& rs, const std::vector<f
         cur.swap(nxt);
         items.swap(nitems);
     }
+    return RT_OK;
 }
 
 // The whole tree in the sequential build's breadth-first numbering: a node's index is its
@@ -296,27 +312,57 @@ extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd
         // on a few threads (RT_KD_THREADS, default up to 8; 1: all on this thread).  The merge
         // renumbers everything breadth first, so the tree is byte-identical either way.
         unsigned n_thr = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
-        if (const char* e = std::getenv("RT_KD_THREADS")) n_thr = (unsigned)std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("RT_DEBUG_KD_THREADS")) n_thr = (unsigned)std::max(1, std::atoi(e));
         if (root.size() < 4096) n_thr = 1;
         const uint32_t STOP = n_thr > 1 ? 4u : UINT32_MAX;
-        SubTree top;
-        std::vector<Frontier> frontier;
-        build_subtree(rs, cen, std::move(root), 0, max_depth, STOP, &top, n_thr > 1 ? &frontier : nullptr);
-        std::vector<SubTree> subs(frontier.size());
-        std::atomic<uint32_t> next{0};
-        auto work = [&]() {
-            for (uint32_t k; (k = next.fetch_add(1)) < frontier.size();)
-                build_subtree(rs, cen, std::move(frontier[k].elems), frontier[k].depth, max_depth, 0, &subs[k], nullptr);
-        };
-        std::vector<std::thread> pool;
-        for (unsigned t = 1; t < n_thr && t < frontier.size(); ++t) pool.emplace_back(work);
-        work();
-        for (auto& th : pool) th.join();
-        max_leaf_depth = top.max_leaf_depth;
-        for (const SubTree& t : subs) max_leaf_depth = std::max(max_leaf_depth, t.max_leaf_depth);
-        if ((st = merge_bfs(top, subs, kt))) { delete kt; return st; }
+        // Nothing throws across the ABI: an allocation failure inside a worker (std::bad_alloc,
+        // std::length_error) or a thread that cannot start becomes RT_ERR_OOM / fewer threads.
+        BuildBudget budget;
+        std::atomic<int> status{RT_OK};
+        try {
+            SubTree top;
+            std::vector<Frontier> frontier;
+            st = build_subtree(rs, cen, std::move(root), 0, max_depth, STOP, &top, n_thr > 1 ? &frontier : nullptr,
+                               &budget);
+            if (st) { delete kt; return st; }
+            std::vector<SubTree> subs(frontier.size());
+            std::atomic<uint32_t> next{0};
+            auto work = [&]() {
+                try {
+                    for (uint32_t k; status.load() == RT_OK && (k = next.fetch_add(1)) < frontier.size();) {
+                        const int r = build_subtree(rs, cen, std::move(frontier[k].elems), frontier[k].depth, max_depth,
+                                                    0, &subs[k], nullptr, &budget);
+                        if (r) status = r;
+                    }
+                } catch (...) {
+                    status = RT_ERR_OOM;
+                }
+            };
+            std::vector<std::thread> pool;
+            for (unsigned t = 1; t < n_thr && t < frontier.size(); ++t) {
+                try {
+                    pool.emplace_back(work);
+                } catch (...) {
+                    break;  // run with the threads that started (the caller's thread always works)
+                }
+            }
+            work();
+            for (auto& th : pool) th.join();
+            if ((st = status.load())) { delete kt; return st; }
+            max_leaf_depth = top.max_leaf_depth;
+            for (const SubTree& t : subs) max_leaf_depth = std::max(max_leaf_depth, t.max_leaf_depth);
+            st = merge_bfs(top, subs, kt);
+        } catch (...) {
+            st = RT_ERR_OOM;
+        }
+        if (st) { delete kt; return st; }
     }
-    kt->nodes = relayout_blocked(kt->nodes);
+    try {
+        kt->nodes = relayout_blocked(kt->nodes);
+    } catch (...) {
+        delete kt;
+        return RT_ERR_OOM;
+    }
     if (kt->nodes.size() >= (1u << 30)) { delete kt; return RT_ERR_OOM; }
     kt->pub.n_nodes = (uint32_t)kt->nodes.size();
     kt->pub.n_refs = (uint32_t)kt->refs.size();

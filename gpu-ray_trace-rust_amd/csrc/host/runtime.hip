@@ -34,7 +34,7 @@ using namespace rth;
 // Radiance buffer cap per queue launch (floats): 16 GiB of 288 GB HBM, so a 1000-spp step of a
 // 1200x600 frame (8.6 GB) is one launch.  Every launch ends in a drain tail (lanes idle while the
 // last paths finish): walled's bench step ran 3.4% faster as one launch than as three of 334 spp
-// (4 GiB cap).  RT_QUEUE_RADIANCE_GIB overrides it; only what a launch needs is allocated.
+// (4 GiB cap).  RT_DEBUG_RADIANCE_GIB overrides it; only what a launch needs is allocated.
 static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 
 // Overlapped queue launches rotate over pipeline slots, each with its own stream, radiance
@@ -57,8 +57,8 @@ static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 // 356; 8 slots, 1/4 grid 370 (1/6: 350, 1/8: 318); 12 slots, 1/6 389, 1/8 400, 1/10 380;
 // biplane / spaceship launches (2 slots) lose with a smaller grid (1/2: -14% / -2%), so they keep
 // the full one.  The first launch of an idle pipeline (and every synchronous call) keeps the full
-// grid too.  RT_PIPELINE_SLOTS (2-32) and RT_QUEUE_GRID_DIV (1-64) override.
-constexpr int N_SLOTS = 32;          // slots a context holds (RT_PIPELINE_SLOTS up to this)
+// grid too.  RT_DEBUG_PIPELINE_SLOTS (2-32) and RT_DEBUG_GRID_DIV (1-64) override.
+constexpr int N_SLOTS = 32;          // slots a context holds (RT_DEBUG_PIPELINE_SLOTS up to this)
 // A launch's item counters: one 128-B line per shard of its items (trace.hip RT_QSHARDS, <= 32)
 constexpr size_t QUEUE_BYTES = 32 * 128;
 static uint32_t slots_for_queues(int hw_queues) {
@@ -105,7 +105,7 @@ struct rt_ctx {
     uint32_t d_tiles_cap = 0;
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
     uint4* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
-    uint32_t pix_block = 1;           // RT_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
+    uint32_t pix_block = 1;           // RT_DEBUG_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
     float4* d_out = nullptr;
@@ -113,16 +113,17 @@ struct rt_ctx {
     DevCounts* d_counts = nullptr;
     uint64_t lane_capacity = 0;   // lanes resident at the kernel's occupancy
     uint32_t n_cu = 0;
-    uint32_t forced_k = 0;        // RT_LANES_PER_PIXEL (tests / tuning)
-    int sched = 0;                // RT_SCHED: 0 auto, 1 direct, 2 queue
-    uint64_t queue_floats = 0;    // RT_QUEUE_RADIANCE_GIB: radiance buffer cap per queue launch
-    bool overlap = true;          // RT_PIPELINE: launch i + 1 may start during launch i's drain
+    uint32_t forced_k = 0;        // RT_DEBUG_LANES_PER_PIXEL (tests / tuning)
+    int sched = 0;                // RT_DEBUG_SCHED: 0 auto, 1 direct, 2 queue
+    uint64_t queue_floats = 0;    // RT_DEBUG_RADIANCE_GIB: radiance buffer cap per queue launch
+    bool overlap = true;          // RT_DEBUG_PIPELINE: launch i + 1 may start during launch i's drain
     uint64_t overlap_max_items = 1ull << 27;  // ... when it has at most this many samples
-    uint32_t n_slots = 0;         // RT_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
+    uint32_t n_slots = 0;         // RT_DEBUG_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
     uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
-    uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_SMALL_LAUNCH_ITEMS: launches this size or less are small
-    uint32_t grid_div = 1;        // small launches behind a busy pipeline: 1/grid_div of the resident grid
-    uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_QUEUE_SHARDS)
+    uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_DEBUG_SMALL_LAUNCH_ITEMS: launches this size or less are small
+    uint32_t grid_div = 0;        // RT_DEBUG_GRID_DIV; 0: small_grid_div(the launch's slots)
+    uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_DEBUG_QUEUE_SHARDS)
+    uint64_t group_items = 0;     // rt_render_to_target: samples per batch group (RT_DEBUG_GROUP_ITEMS; 0: GROUP_ITEMS)
     float last_ms = 0.f;
     std::string err;
 };
@@ -141,9 +142,32 @@ static int set_err(rt_ctx* c, int code, const std::string& msg) {
     return code;
 }
 
+// Nothing throws across the C ABI: a host allocation failure (std::bad_alloc from a vector of the
+// scene's size) or a thread that cannot start becomes a status code.
+template <class F>
+static int guarded(rt_ctx* c, F f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return set_err(c, RT_ERR_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return set_err(c, RT_ERR_OOM, std::string("host runtime: ") + e.what());
+    }
+}
+
 #ifndef RT_PIX_BLOCK
 #define RT_PIX_BLOCK 8  // queue order of a launch's pixels: B x B blocks of each tile (1: row order)
 #endif
+
+// A/B and test knobs, read here and nowhere else, all named RT_DEBUG_<name> (INTEGRATION.md
+// lists them).  A caller needs none of them: each selects an alternative schedule or layout that
+// the GPU tests check bit-invariant against the oracle.  The one other variable the library reads
+// is HIP's own GPU_MAX_HW_QUEUES (the hardware queues the launch pipeline can use).
+static const char* debug_env(const char* name) {
+    char key[64];
+    std::snprintf(key, sizeof key, "RT_DEBUG_%s", name);
+    return std::getenv(key);
+}
 
 template <class T>
 static int upload(rt_ctx* c, const std::vector<T>& v, const T** out) {
@@ -304,9 +328,9 @@ static void destroy_ctx(rt_ctx* c) {
     delete c;
 }
 
-// RT_CREATE_TIMING=1: rt_create prints the wall time of its phases to stderr (tools/host_rates.py).
+// RT_DEBUG_CREATE_TIMING=1: rt_create prints the wall time of its phases to stderr (tools/host_rates.py).
 struct PhaseClock {
-    bool on = std::getenv("RT_CREATE_TIMING") != nullptr;
+    bool on = debug_env("CREATE_TIMING") != nullptr;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     void mark(const char* what) {
         if (!on) return;
@@ -341,7 +365,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     std::vector<uint32_t> t8;
     bool t8_ok = false;
     std::thread packer;
-    if (texel_count && !std::getenv("RT_TEXELS_F32"))
+    if (texel_count && !debug_env("TEXELS_F32"))
         packer = std::thread([&] { t8_ok = pack_texels_u8(scene, texs, texel_count, &t8); });
     struct Join { std::thread& t; ~Join() { if (t.joinable()) t.join(); } } join{packer};
 
@@ -657,37 +681,37 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
     pc.mark("accum_props");
     c->n_cu = (uint32_t)prop.multiProcessorCount;
-    if (const char* e = std::getenv("RT_SCHED")) {
+    if (const char* e = debug_env("SCHED")) {
         if (!std::strcmp(e, "direct")) c->sched = 1;
         else if (!std::strcmp(e, "queue")) c->sched = 2;
     }
-    if (const char* e = std::getenv("RT_LANES_PER_PIXEL")) {
+    if (const char* e = debug_env("LANES_PER_PIXEL")) {
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
     }
     c->queue_floats = QUEUE_RADIANCE_FLOATS;
-    if (const char* e = std::getenv("RT_QUEUE_RADIANCE_GIB")) {
+    if (const char* e = debug_env("RADIANCE_GIB")) {
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->queue_floats = (uint64_t)v << 28;
     }
     // Traversal of the queue kernels: the reference's stack (kdtree.rs:66-104) or stackless
     // kd-restart with push-down, bit-identical (trace.hip stack_search_coop).  The stack is faster
     // on the mesh scenes; the sphere-only kernel, which descends for 0.05 nodes
-    // per sample, runs stackless and needs no global stack.  RT_KD_RESTART=0/1 overrides.
-    // RT_KD_RESTART=2: stackless with the wave's leaf triangles staged in LDS per round (the
+    // per sample, runs stackless and needs no global stack.  RT_DEBUG_KD_RESTART=0/1 overrides.
+    // RT_DEBUG_KD_RESTART=2: stackless with the wave's leaf triangles staged in LDS per round (the
     // general kernel; measured slower).
     // Camera-ray packets in the general queue kernel (trace.hip closest_packet), bit-identical to
-    // the cooperative search; RT_PACKET=0 turns them off.  RT_PIX_BLOCK=1 gives the queue the
+    // the cooperative search; RT_DEBUG_PACKET=0 turns them off.  RT_DEBUG_PIX_BLOCK=1 gives the queue the
     // launch pixels in row order instead of 8 x 8 blocks (the same images).
     d.packet = 1u;
-    if (const char* e = std::getenv("RT_PACKET")) d.packet = std::strcmp(e, "0") ? 1u : 0u;
+    if (const char* e = debug_env("PACKET")) d.packet = std::strcmp(e, "0") ? 1u : 0u;
     c->pix_block = RT_PIX_BLOCK;
-    if (const char* e = std::getenv("RT_PIX_BLOCK")) {
+    if (const char* e = debug_env("PIX_BLOCK")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->pix_block = (uint32_t)v;
     }
     d.restart = d.spheres_only ? 1u : 0u;
-    if (const char* e = std::getenv("RT_KD_RESTART")) {
+    if (const char* e = debug_env("KD_RESTART")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         d.restart = v > 2 ? 1u : (uint32_t)v;
     }
@@ -695,9 +719,9 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     // launches (8-10 ms tails) and small sphere-only ones — walled's ~0.4 ms tail on
     // one rank's 90 M-sample share at N = 8 (9 ms): +3% overlapped, while at 180 M it is neutral
     // and at 360 / 720 M a fold beside the next trace grid costs 1%.  enqueue_queue overlaps
-    // launches of at most overlap_max_items (2^27) samples.  RT_PIPELINE=0/1/2 overrides.
+    // launches of at most overlap_max_items (2^27) samples.  RT_DEBUG_PIPELINE=0/1/2 overrides.
     c->overlap = true;
-    if (const char* e = std::getenv("RT_PIPELINE_SLOTS")) {
+    if (const char* e = debug_env("PIPELINE_SLOTS")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 2 && v <= (unsigned long)N_SLOTS) c->n_slots = (uint32_t)v;
     }
@@ -705,22 +729,22 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const char* q = std::getenv("GPU_MAX_HW_QUEUES");  // what HIP read when it started
         const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
         c->small_slots = slots_for_queues(hwq);
-        c->grid_div = small_grid_div(c->small_slots);
     }
-    if (const char* e = std::getenv("RT_QUEUE_SHARDS")) {
+    if (const char* e = debug_env("QUEUE_SHARDS")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 32) c->queue_shards = (uint32_t)v;
     }
-    if (const char* e = std::getenv("RT_SMALL_LAUNCH_ITEMS")) c->small_items = std::strtoull(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_QUEUE_GRID_DIV")) {
+    if (const char* e = debug_env("SMALL_LAUNCH_ITEMS")) c->small_items = std::strtoull(e, nullptr, 10);
+    if (const char* e = debug_env("GROUP_ITEMS")) c->group_items = std::strtoull(e, nullptr, 10);
+    if (const char* e = debug_env("GRID_DIV")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->grid_div = (uint32_t)v;
     }
-    if (const char* e = std::getenv("RT_PIPELINE")) {  // 0: never, 1: below the item limit, 2: always
+    if (const char* e = debug_env("PIPELINE")) {  // 0: never, 1: below the item limit, 2: always
         c->overlap = std::strcmp(e, "0") != 0;
         if (!std::strcmp(e, "2")) c->overlap_max_items = ~0ull;
     }
-    if (const char* e = std::getenv("RT_QUEUE_RADIANCE_FLOATS")) {  // tests: force split launches
+    if (const char* e = debug_env("RADIANCE_FLOATS")) {  // tests: force split launches
         unsigned long long v = std::strtoull(e, nullptr, 10);
         if (v >= 3 && v <= (1ull << 34)) c->queue_floats = (uint64_t)v;
     }
@@ -737,7 +761,7 @@ extern "C" int rt_create(const rt_scene_desc* scene, const rt_camera* cam, const
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return RT_ERR_OOM;
     c->device = device;
-    int st = create_impl(c, scene, cam, info, tree);
+    int st = guarded(c, [&] { return create_impl(c, scene, cam, info, tree); });
     if (st) {
         std::fprintf(stderr, "rt_create: %s\n", c->err.c_str());
         destroy_ctx(c);
@@ -922,8 +946,8 @@ static int ensure_radiance(rt_ctx* c, Slot& sl, uint64_t floats) {
 static constexpr uint32_t SAMPLES_PER_LANE_CHUNK = 64;
 
 // Schedule: the queue (persistent lanes over (pixel, sample) items, tools/variant_bench.py:
-// walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_SCHED=direct or
-// RT_LANES_PER_PIXEL asks for the direct one-lane-per-pixel schedule (kept for A/B and as the
+// walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_DEBUG_SCHED=direct or
+// RT_DEBUG_LANES_PER_PIXEL asks for the direct one-lane-per-pixel schedule (kept for A/B and as the
 // tests' second path).
 static bool use_queue(const rt_ctx* c) {
     if (c->forced_k) return false;
@@ -936,8 +960,18 @@ static bool use_queue(const rt_ctx* c) {
 // chunk's fold (accumulator order, draw_scene.rs:81-83) and, when given, for `after` (the
 // caller's stream: its readers of `out` from the previous call).  Returns with the last fold
 // in c->last_fold.
+//
+// Batches (rt_render_batches_device_async, rt_render_to_target): the call's samples are
+// consecutive batches of `batch` samples, and batch k's frame goes to outs[k] (nullptr: none).
+// The trace launches are the call's, whatever the batches; after each one the fold runs batch by
+// batch — one fold kernel per batch part inside the launch, in sample order — and the fold that
+// completes batch k writes outs[k].  A fold part reads its rows of the launch's radiance buffer
+// ([sample][pixel], so a part is a contiguous block) and continues the running mean exactly where
+// the previous part left it: the frames are those of one call per batch, bit for bit.  Chunks of
+// a call with several batches hold whole batches when a batch fits the radiance cap.
 static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sample_begin,
-                         uint32_t sample_count, hipEvent_t after) {
+                         uint32_t sample_count, hipEvent_t after, uint32_t batch, float4* const* outs) {
+    if (batch == 0 || batch > sample_count) batch = sample_count ? sample_count : 1u;
     uint64_t chunk = c->queue_floats / (3 * n_out);
     if (chunk < 1) chunk = 1;
     if (chunk > sample_count) chunk = sample_count ? sample_count : 1;
@@ -948,7 +982,12 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
     // the counter overshoots n_items by at most one grab (<= 1024 = 16 x 64) per wave
     if (n_out * chunk + lanes * 16 >= (1ull << 32)) chunk = ((1ull << 32) - lanes * 16 - 1) / n_out;
     if (chunk < 1) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels for one launch");
-    if (sample_count > chunk) {  // equal launches: ceil(count / n) samples each
+    if (sample_count > chunk && batch < sample_count && chunk >= batch) {
+        // whole batches per launch, in equal launches of ceil(n_batches / n) batches
+        const uint64_t nb = sample_count / batch, per = chunk / batch;
+        const uint64_t n = (nb + per - 1) / per;
+        chunk = batch * ((nb + n - 1) / n);
+    } else if (sample_count > chunk) {  // equal launches: ceil(count / n) samples each
         const uint64_t n = (sample_count + chunk - 1) / chunk;
         chunk = (sample_count + n - 1) / n;
     }
@@ -967,9 +1006,20 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         const bool overlap = c->overlap && a.n_items <= c->overlap_max_items;
         const bool small = a.n_items <= c->small_items;
         // a small launch behind a launch still running takes a share of the grid (see N_SLOTS)
-        const bool busy = c->last_fold && hipEventQuery(c->last_fold) == hipErrorNotReady;
-        (void)hipGetLastError();  // a not-ready query is no error for the launch checks below
+        bool busy = false;
+        if (c->last_fold) {
+            const hipError_t q = hipEventQuery(c->last_fold);
+            if (q == hipErrorNotReady) {
+                busy = true;
+                (void)hipGetLastError();  // clear the not-ready status only (every earlier call was checked)
+            } else if (q != hipSuccess) {  // e.g. a faulted earlier launch: report it, do not launch
+                (void)hipGetLastError();   // reported here, not again by a later call's launch check
+                return set_err(c, RT_ERR_HIP, std::string("hipEventQuery(last fold): ") + hipGetErrorString(q));
+            }
+        }
         const uint32_t n_slots = c->n_slots ? c->n_slots : (small ? c->small_slots : 2u);
+        // the grid share follows the slots this launch rotates over (RT_DEBUG_GRID_DIV overrides)
+        const uint32_t grid_div = c->grid_div ? c->grid_div : small_grid_div(n_slots);
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
         for (uint32_t k = 0; k < (overlap ? n_slots : 1u); ++k) {
             const int e = ensure_slot(c, overlap ? k : c->cur_slot);
@@ -1002,14 +1052,28 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
             HIPCHK(c, hipMemsetAsync(sl.queue, 0, QUEUE_BYTES, sl.stream));
             if ((st = record_launch_event(c, true, sl.stream))) return st;
             uint32_t nb = (uint32_t)(lanes / BLOCK);
-            if (overlap && small && busy && c->grid_div > 1)
-                nb = nb / c->grid_div > (uint32_t)c->n_cu ? nb / c->grid_div : (uint32_t)c->n_cu;
+            if (overlap && small && busy && grid_div > 1)
+                nb = nb / grid_div > (uint32_t)c->n_cu ? nb / grid_div : (uint32_t)c->n_cu;
             HIPCHK(c, launch_trace_queue(a, nb, sl.stream));
             if ((st = record_launch_event(c, false, sl.stream))) return st;
         }
         if (c->last_fold && c->last_fold != sl.fold_done) HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));
         if (after) HIPCHK(c, hipStreamWaitEvent(sl.stream, after, 0));
-        HIPCHK(c, launch_fold(a, sl.stream));
+        // the fold, batch part by batch part (one part when the launch is inside one batch)
+        const uint64_t cb = a.sample_begin, ce = cb + a.sample_count;
+        uint64_t fs = cb;
+        do {
+            const uint64_t k = (fs - sample_begin) / batch;
+            const uint64_t be = sample_begin + (k + 1) * batch;
+            const uint64_t fe = ce < be ? ce : be;
+            LaunchArgs f = a;
+            f.sample_begin = fs;
+            f.sample_count = (uint32_t)(fe - fs);
+            f.radiance = a.radiance + 3 * n_out * (fs - cb);
+            f.out = (fe == be || fe == sample_begin + sample_count) ? outs[k] : nullptr;
+            HIPCHK(c, launch_fold(f, sl.stream));
+            fs = fe;
+        } while (fs < ce);
         HIPCHK(c, hipEventRecord(sl.fold_done, sl.stream));
         c->last_fold = sl.fold_done;
         done += a.sample_count;
@@ -1058,8 +1122,14 @@ static int run_direct(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint32_t K, uint6
 
 // Enqueues one rt_render* call.  `after`: an event the output writers must wait for.  `range`:
 // the mean over this call's samples alone (rt_render_range), in accum_range.
+static int render_impl_(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                        uint32_t sample_count, float4* dev_out, hipEvent_t after, bool range);
 static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
                        uint32_t sample_count, float4* dev_out, hipEvent_t after, bool range = false) {
+    return guarded(c, [&] { return render_impl_(c, tiles, n_tiles, sample_begin, sample_count, dev_out, after, range); });
+}
+static int render_impl_(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                        uint32_t sample_count, float4* dev_out, hipEvent_t after, bool range) {
     LaunchArgs a{};
     uint64_t n_out = 0;
     const uint32_t K = choose_k(c, tile_pixels(tiles, n_tiles));
@@ -1078,7 +1148,31 @@ static int render_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64
     }
     if (!use_queue(c)) return run_direct(c, a, n_out, K, sample_begin, sample_count);
     open_window(c);
-    return enqueue_queue(c, a, n_out, sample_begin, sample_count, after);
+    return enqueue_queue(c, a, n_out, sample_begin, sample_count, after, sample_count, &dev_out);
+}
+
+// n_batches consecutive batches of `batch` samples from sample_begin, batch k's frame into outs[k]
+// (enqueue_queue's fold parts); the direct schedule renders them one call at a time.
+static int render_batches_impl(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint64_t sample_begin,
+                               uint32_t batch, uint32_t n_batches, float4* const* outs, hipEvent_t after) {
+    if (n_batches == 0) return RT_OK;
+    if (batch == 0 || (uint64_t)batch * n_batches >= (1ull << 32)) return set_err(c, RT_ERR_INVALID_ARG, "bad batches");
+    if (!use_queue(c)) {
+        for (uint32_t k = 0; k < n_batches; ++k) {
+            const int st = render_impl(c, tiles, n_tiles, sample_begin + (uint64_t)k * batch, batch, outs[k], after);
+            if (st) return st;
+        }
+        return RT_OK;
+    }
+    return guarded(c, [&]() -> int {
+        LaunchArgs a{};
+        uint64_t n_out = 0;
+        int st = prepare_tiles(c, tiles, n_tiles, 1, &a, &n_out);
+        if (st) return st;
+        a.out = nullptr;
+        open_window(c);
+        return enqueue_queue(c, a, n_out, sample_begin, batch * n_batches, after, batch, outs);
+    });
 }
 
 static int ensure_out(rt_ctx* c, uint64_t n) {
@@ -1138,6 +1232,20 @@ extern "C" int rt_render_device_async(rt_ctx* c, const rt_tile* tiles, uint32_t 
     if (st) return st;
     // and the caller's later work sees the finished output
     HIPCHK(c, hipStreamWaitEvent(cs, c->last_fold, 0));
+    return RT_OK;
+}
+
+extern "C" int rt_render_batches_device_async(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles,
+                                              uint64_t sample_begin, uint32_t batch, uint32_t n_batches,
+                                              float* const* outs_dev, void* stream) {
+    if (!c || !tiles || !outs_dev || batch == 0) return RT_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    HIPCHK(c, hipEventRecord(c->caller_ev, cs));
+    int st = render_batches_impl(c, tiles, n_tiles, sample_begin, batch, n_batches,
+                                 reinterpret_cast<float4* const*>(outs_dev), c->caller_ev);
+    if (st) return st;
+    if (c->last_fold) HIPCHK(c, hipStreamWaitEvent(cs, c->last_fold, 0));
     return RT_OK;
 }
 
@@ -1215,10 +1323,16 @@ extern "C" int rt_destroy(rt_ctx* c) {
     return RT_OK;
 }
 
-// render_to_target_gpu (draw_scene.rs:17-47) on one device: spp/batch launches over the whole
-// frame; after each, the RGBA8 target is refreshed and the update hook runs.  Pipelined: batch
-// i + 1 is enqueued before batch i's frame is read back, converted and handed to the hook, so
-// the device never waits on the host and launch i + 1 fills launch i's drain tail.
+// render_to_target_gpu (draw_scene.rs:17-47) on one device: spp/batch batches over the whole
+// frame; after each, the RGBA8 target is refreshed and the update hook runs, in batch order.
+// Consecutive batches are traced together (render_batches_impl): a group of G batches is one
+// trace launch of at least GROUP_ITEMS samples, folded batch by batch, so a small batch (a380's
+// gpu_render_batch of 1 spp: 0.72 M samples, ~2 ms of work against a ~10 ms drain tail) no longer
+// needs a pipeline slot, and a hardware queue, of its own: the throughput does not depend on the
+// caller's GPU_MAX_HW_QUEUES.  Pipelined: group g + 1 is enqueued before group g's frames are
+// read back, converted and handed to the hook, so the device never waits on the host and group
+// g + 1's launch fills group g's drain tail.  The frames are those of one launch per batch.
+constexpr uint64_t GROUP_ITEMS = 1ull << 24;
 extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* cam,
                                    const rt_render_info* info, uint32_t spp, uint32_t batch, int device,
                                    uint8_t* target, rt_update_hook hook, void* user) {
@@ -1229,46 +1343,50 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
     if (st) return st;
     const rt_tile full{0, 0, info->width, info->height};
     const uint64_t npix = (uint64_t)info->width * info->height;
-    std::vector<float> rgba(npix * 4);
-    // Batches in flight: batch i + AHEAD is enqueued before batch i is read back, each into its
-    // own output buffer, so the launch pipeline's slots stay busy (a 1-spp batch holds ~2 ms of
-    // work against a ~10 ms drain tail); the hook still sees every batch, in order.
-    const uint32_t AHEAD = (npix * batch <= c->small_items ? c->small_slots : 8u) - 1u;
     const uint32_t n_batch = spp / batch;
-    const uint32_t ring = std::min(AHEAD, n_batch ? n_batch - 1u : 0u) + 1u;
-    std::vector<float4*> dbuf(ring, nullptr);
-    std::vector<hipEvent_t> done(ring, nullptr);
+    const uint64_t per_batch = npix * batch;
+    const uint64_t group_items = c->group_items ? c->group_items : GROUP_ITEMS;
+    const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_batch, group_items / per_batch));
+    // groups in flight beyond the one being read back: a small group launch rotates over the
+    // small-launch slots, a larger one over two
+    const uint32_t ahead = (c->n_slots ? c->n_slots : (per_batch * G <= c->small_items ? c->small_slots : 2u)) - 1u;
+    const uint32_t ring = (uint32_t)std::min<uint64_t>(n_batch, (uint64_t)G * (ahead + 1));
+    std::vector<float4*> dbuf;
+    std::vector<hipEvent_t> done;
     auto run = [&]() -> int {
+        std::vector<float> rgba(npix * 4);
+        dbuf.assign(ring, nullptr);
+        done.assign(ring, nullptr);
         for (uint32_t k = 0; k < ring; ++k) {
             if (hipMalloc(&dbuf[k], npix * sizeof(float4)) != hipSuccess) return set_err(c, RT_ERR_OOM, "output alloc failed");
             HIPCHK(c, hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
         }
-        auto deliver = [&](uint32_t b) -> int {  // batch b's frame: samples [0, (b + 1) * batch)
-            const uint32_t k = b % ring;
-            HIPCHK(c, hipEventSynchronize(done[k]));
-            HIPCHK(c, hipMemcpy(rgba.data(), dbuf[k], npix * sizeof(float4), hipMemcpyDeviceToHost));
-            rt_rgba_to_u8(rgba.data(), npix, target);
-            if (hook) hook(user, (b + 1) * batch);
+        uint32_t delivered = 0;
+        auto deliver_to = [&](uint32_t end) -> int {  // batches [delivered, end), in order
+            for (; delivered < end; ++delivered) {  // batch b's frame: samples [0, (b + 1) * batch)
+                const uint32_t k = delivered % ring;
+                HIPCHK(c, hipEventSynchronize(done[k]));
+                HIPCHK(c, hipMemcpy(rgba.data(), dbuf[k], npix * sizeof(float4), hipMemcpyDeviceToHost));
+                rt_rgba_to_u8(rgba.data(), npix, target);
+                if (hook) hook(user, (delivered + 1) * batch);
+            }
             return RT_OK;
         };
-        for (uint32_t i = 0; i < n_batch; ++i) {
-            if (i >= ring) {  // its buffer's previous batch first
-                int r = deliver(i - ring);
-                if (r) return r;
-            }
-            int r = render_impl(c, &full, 1, i * batch, batch, dbuf[i % ring], nullptr);
+        std::vector<float4*> outs(G);
+        for (uint32_t g0 = 0; g0 < n_batch; g0 += G) {
+            const uint32_t gn = std::min(G, n_batch - g0);
+            // the buffers this group reuses hold batches g0 + gn - 1 - ring and earlier
+            int r = deliver_to(g0 + gn > ring ? g0 + gn - ring : 0u);
             if (r) return r;
-            HIPCHK(c, hipEventRecord(done[i % ring], c->slot[c->cur_slot].stream));
+            for (uint32_t k = 0; k < gn; ++k) outs[k] = dbuf[(g0 + k) % ring];
+            if ((r = render_batches_impl(c, &full, 1, (uint64_t)g0 * batch, batch, gn, outs.data(), nullptr))) return r;
+            for (uint32_t k = 0; k < gn; ++k) HIPCHK(c, hipEventRecord(done[(g0 + k) % ring], c->slot[c->cur_slot].stream));
         }
-        for (uint32_t b = n_batch > ring ? n_batch - ring : 0u; b < n_batch; ++b) {
-            int r = deliver(b);
-            if (r) return r;
-        }
-        return RT_OK;
+        return deliver_to(n_batch);
     };
-    st = run();
+    st = guarded(c, run);
     if (!st) st = sync_all(c);
-    for (uint32_t k = 0; k < ring; ++k) {
+    for (size_t k = 0; k < dbuf.size(); ++k) {
         if (done[k]) (void)hipEventDestroy(done[k]);
         if (dbuf[k]) {
             (void)sync_all(c);

@@ -1,0 +1,125 @@
+// diag.h — diagnostic instrumentation of the queue kernels, kept out of the shipped library.
+//
+// The product build (make) defines neither switch: every DIAG_* / TM_* / VC macro below expands
+// to nothing, so the shipped code object holds no clock reads, no instrumentation atomics and no
+// printf (tests/test_device_code.py checks the last).  `make diag` builds
+// lib/variants/librt_diag_timing.so (-DRT_TIMING=1) and lib/variants/librt_diag_vmem.so
+// (-DRT_VMEM_COUNT=1) for the tools that read their printed lines:
+//   RT_TIMING      wave-clock split of the queue kernels, summed over waves and printed by the
+//                  last wave of each launch (tools/gpu_timing.sh);
+//   RT_VMEM_COUNT  vector-memory load instructions of the general queue kernel by class, counted
+//                  once per wave execution of each load site (tools/vmem_classes.py).  Classes:
+//                  0 descent nodes, 1 pop nodes, 2 pass refs, 3 pass triangles, 4 leading spheres,
+//                  5 winner re-test, 6 path-start pixel table, 7 mesh shading records, 8 textures,
+//                  9 sphere / free-triangle shading, 10 packet leaf visits (scalar loads: no
+//                  VMEM), 11 cooperative passes, 12 cooperative rounds, 13 radiance stores
+//                  (writes), 14 path starts, 15-21 leaf sharing per round.
+// Included by trace.hip after the kernel helpers it calls (wave_incl_scan).
+#pragma once
+
+#ifndef RT_TIMING
+#define RT_TIMING 0
+#endif
+#ifndef RT_VMEM_COUNT
+#define RT_VMEM_COUNT 0
+#endif
+
+namespace rtd {
+
+#if RT_TIMING
+__device__ unsigned long long g_tm[16];
+__device__ unsigned int g_tm_waves;
+__device__ __forceinline__ unsigned long long tm_now() {  // ordered stamp (cdna guide §7)
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define TM_NOW() ::rtd::tm_now()
+#define TM_ADD(i, v) do { const unsigned long long tm_v_ = (unsigned long long)(v); \
+                          if (__lane_id() == 0) atomicAdd(&::rtd::g_tm[i], tm_v_); } while (0)
+#define TM_VAR(decl) decl
+#else
+#define TM_ADD(i, v) do { } while (0)
+#define TM_VAR(decl)
+#endif
+
+#if RT_VMEM_COUNT
+__device__ unsigned long long g_vc[24];
+__device__ unsigned int g_vc_waves;
+#define VC(i, n) do { if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
+                           atomicAdd(&::rtd::g_vc[i], (unsigned long long)(n)); } while (0)
+#else
+#define VC(i, n) do { } while (0)
+#endif
+
+#if RT_TIMING || RT_VMEM_COUNT
+// One cooperative round, before its passes: how many lanes share a leaf.  RT_TIMING counts the
+// rounds, the lanes with a leaf and the lanes at the first such lane's leaf; RT_VMEM_COUNT the
+// pairs at leaves held by 2+ / 3+ / 4+ / 8+ lanes.
+__device__ __forceinline__ void diag_round_sharing(uint32_t off, uint32_t cnt) {
+#if RT_TIMING
+    TM_ADD(9, 1);
+    TM_ADD(10, __popcll(__ballot(cnt > 0)));
+    {
+        const uint64_t hv = __ballot(cnt > 0);
+        const uint32_t f = hv ? (uint32_t)__ffsll((unsigned long long)hv) - 1u : 0u;
+        const uint32_t fo = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)f);
+        TM_ADD(11, hv ? __popcll(__ballot(cnt > 0 && off == fo)) : 0);
+    }
+#endif
+#if RT_VMEM_COUNT
+    uint64_t pending = __ballot(cnt > 0);
+    while (pending) {
+        const uint32_t ld = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
+        const uint32_t o = __builtin_amdgcn_readlane(off, ld), n = __builtin_amdgcn_readlane(cnt, ld);
+        const uint64_t same = __ballot(off == o && cnt > 0) & pending;
+        pending &= ~same;
+        const uint32_t g = (uint32_t)__popcll(same);
+        VC(15, n * g);
+        if (g >= 2) VC(16, n * g);
+        if (g >= 3) VC(17, n * g);
+        if (g >= 4) VC(18, n * g);
+        if (g >= 8) VC(19, n * g);
+        VC(20, n * ((g + 3u) / 4u));
+        VC(21, 1);
+    }
+#endif
+}
+#define DIAG_ROUND_SHARING(off, cnt) ::rtd::diag_round_sharing(off, cnt)
+#else
+#define DIAG_ROUND_SHARING(off, cnt) do { } while (0)
+#endif
+
+// The last wave of a launch prints the launch's totals and clears them for the next launch.
+#if RT_TIMING || RT_VMEM_COUNT
+template <bool GEN>
+__device__ __forceinline__ void diag_wave_exit() {
+#if RT_VMEM_COUNT
+    if (GEN && __lane_id() == 0 && atomicAdd(&g_vc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+        __threadfence();
+        for (int i = 0; i < 24; ++i) printf("RT_VC %d %llu\n", i, g_vc[i]);
+        for (int i = 0; i < 24; ++i) g_vc[i] = 0;
+        g_vc_waves = 0;
+    }
+#endif
+#if RT_TIMING
+    if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+        __threadfence();
+        printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
+               "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu | "
+               "passes_time %llu passes %llu\n",
+               g_tm[0], g_tm[1], g_tm[2], g_tm[3], g_tm[4], g_tm[5], g_tm[6], g_tm[7], g_tm[8], g_tm[9],
+               g_tm[10], g_tm[11], g_tm[12], g_tm[13]);
+        for (int i = 0; i < 16; ++i) g_tm[i] = 0;
+        g_tm_waves = 0;
+    }
+#endif
+}
+#define DIAG_WAVE_EXIT(GEN) ::rtd::diag_wave_exit<GEN>()
+#else
+#define DIAG_WAVE_EXIT(GEN) do { } while (0)
+#endif
+
+}  // namespace rtd

@@ -32,6 +32,7 @@
 #include "../../../include/rt_rng.h"
 #include "../../../include/rt_libm.h"
 #include "device_scene.h"
+#include "diag.h"  // instrumentation of the diagnostic builds only (make diag); empty here
 
 #ifndef RT_REGEN_MIN
 #define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
@@ -86,47 +87,6 @@ constexpr float RR_THRES = 0.4f;        // radiance.rs:77
 // with p = 0.4, so a cap of 1024 bounces changes an estimate with probability < 0.4^1000.
 // It only guarantees that a corrupted scene cannot hang the GPU.
 constexpr int MAX_BOUNCES = 1024;
-
-// Diagnostic build only (-DRT_TIMING=1, tools/build_variants.sh): wave-clock split of the general
-// queue kernel, summed over waves and printed by the last wave of each launch.
-#ifndef RT_TIMING
-#define RT_TIMING 0
-#endif
-#if RT_TIMING
-__device__ unsigned long long g_tm[16];
-__device__ unsigned int g_tm_waves;
-__device__ __forceinline__ unsigned long long tm_now() {  // ordered stamp (cdna guide §7)
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define TM_NOW() tm_now()
-#define TM_ADD(i, v) do { const unsigned long long tm_v_ = (unsigned long long)(v); if (__lane_id() == 0) atomicAdd(&g_tm[i], tm_v_); } while (0)
-#else
-#define TM_ADD(i, v) do { } while (0)
-#endif
-
-// Diagnostic build only (-DRT_VMEM_COUNT=1): vector-memory load instructions of the general queue
-// kernel by class, counted once per wave execution of each load site (the first active lane adds
-// the site's instruction count to a global counter), printed by the last wave of each launch
-// (tools/vmem_classes.py).  Classes: 0 descent nodes, 1 pop nodes, 2 pass refs, 3 pass triangles,
-// 4 leading spheres, 5 winner re-test, 6 path-start pixel table, 7 mesh shading records,
-// 8 textures, 9 sphere / free-triangle shading, 10 packet leaf visits (scalar loads: no VMEM),
-// 11 cooperative passes, 12 cooperative rounds, 13 radiance stores (writes), 14 path starts.
-#ifndef RT_VMEM_COUNT
-#define RT_VMEM_COUNT 0
-#endif
-#if RT_VMEM_COUNT
-__device__ unsigned long long g_vc[24];
-__device__ unsigned int g_vc_waves;
-#define VC(i, n) do { if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
-                           atomicAdd(&g_vc[i], (unsigned long long)(n)); } while (0)
-#else
-#define VC(i, n) do { } while (0)
-#endif
-
 
 struct V3 {
     float x, y, z;
@@ -1026,43 +986,11 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 cnt -= lead;
             }
         }
-        TM_ADD(9, 1);
-        TM_ADD(10, __popcll(__ballot(cnt > 0)));
-#if RT_TIMING
-        {   // leaf sharing: lanes at the leaf of the first lane with one
-            const uint64_t hv = __ballot(cnt > 0);
-            const uint32_t f = hv ? (uint32_t)__ffsll((unsigned long long)hv) - 1u : 0u;
-            const uint32_t fo = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)f);
-            TM_ADD(11, hv ? __popcll(__ballot(cnt > 0 && off == fo)) : 0);
-        }
-#endif
-#if RT_TIMING
-        const unsigned long long tmc0 = TM_NOW();
-#endif
-#if RT_VMEM_COUNT
-        {   // leaf sharing in this round: groups of lanes at one leaf (equal offsets), their pairs
-            uint64_t pending = __ballot(cnt > 0);
-            while (pending) {
-                const uint32_t ld = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
-                const uint32_t o = __builtin_amdgcn_readlane(off, ld), n = __builtin_amdgcn_readlane(cnt, ld);
-                const uint64_t same = __ballot(off == o && cnt > 0) & pending;
-                pending &= ~same;
-                const uint32_t g = (uint32_t)__popcll(same);
-                VC(15, n * g);
-                if (g >= 2) VC(16, n * g);
-                if (g >= 3) VC(17, n * g);
-                if (g >= 4) VC(18, n * g);
-                if (g >= 8) VC(19, n * g);
-                VC(20, n * ((g + 3u) / 4u));
-                VC(21, 1);
-            }
-        }
-#endif
+        DIAG_ROUND_SHARING(off, cnt);
+        TM_VAR(const unsigned long long tmc0 = TM_NOW());
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
-#if RT_TIMING
         TM_ADD(12, TM_NOW() - tmc0);
         TM_ADD(13, (__shfl(wave_incl_scan(cnt, lane), 63) + 63u) / 64u);
-#endif
         if (!done) {
             if (RT_LEAF_REUSE) {
                 prev_list = list;
@@ -1249,9 +1177,7 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     const bool fast = !in || (sc.fastdiv && origin_fast_ok(r.o));
     const bool all_fast = __ballot(!fast) == 0;
     bool pk = false, pk_live = false;
-#if RT_TIMING
-    const unsigned long long tm0 = TM_NOW();
-#endif
+    TM_VAR(const unsigned long long tm0 = TM_NOW());
     if (RT_PACKET && !SLAB && ps && sc.packet) {
         // camera rays of the direction octant of the first one form the packet (NaN directions
         // never: d > 0 and d < 0 are both false); the other lanes take the cooperative search
@@ -1271,22 +1197,18 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
         }
     }
     const bool in_coop = in && (!pk || pk_live);
-#if RT_TIMING
-    const unsigned long long tm1 = TM_NOW();
+    TM_VAR(const unsigned long long tm1 = TM_NOW());
     TM_ADD(0, tm1 - tm0);
     TM_ADD(6, __popcll(__ballot(pk)));
     TM_ADD(7, __popcll(__ballot(pk && pk_live)));
     TM_ADD(8, __popcll(__ballot(in_coop)));
-#endif
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
             found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
         else
             found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
     }
-#if RT_TIMING
     TM_ADD(1, TM_NOW() - tm1);
-#endif
     if (found) return true;
     if (active && sc.has_cube) {
         best->ref = REF_CUBE;
@@ -1897,9 +1819,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                                                                                 const float4* __restrict__ pk_prim4) {
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
-#if RT_TIMING
-    const unsigned long long tm_start = TM_NOW();
-#endif
+    TM_VAR(const unsigned long long tm_start = TM_NOW());
     if (!GEN) {  // only the sphere-only kernel reads the LDS sphere tables
         fill_lds_spheres(sc);
         __syncthreads();
@@ -1921,14 +1841,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     Path p;
     // RT_START_BATCH: the wave's current batch of starts, entries [st_pos, 64) not yet taken
     uint32_t st_pos = 64u, st_n = 0u;
-#if RT_TIMING
-    // sphere-only kernel: wave clock in path starts, normalize, closest hit and shading
-    unsigned long long tq_regen = 0, tq_norm = 0, tq_closest = 0, tq_shade = 0, tq_seg = 0;
-#endif
     for (;;) {
-#if RT_TIMING
-        const unsigned long long tq0 = TM_NOW();
-#endif
         const uint64_t need = __ballot(!have && !done);
         // Starting paths is wave-wide work at the width of the idle lanes: ~10 of 64 lanes end a
         // path per segment, so without batched starts the wave waits for RT_REGEN_MIN of them.
@@ -2048,64 +1961,15 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
                 pool += n;
             }
         }
-#if RT_TIMING
-        tq_regen += TM_NOW() - tq0;
-#endif
         if (__ballot(have) == 0) {
-#if RT_VMEM_COUNT
-            if (GEN && __lane_id() == 0 && atomicAdd(&g_vc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
-                __threadfence();
-                for (int i = 0; i < 24; ++i) printf("RT_VC %d %llu\n", i, g_vc[i]);
-                for (int i = 0; i < 24; ++i) g_vc[i] = 0;
-                g_vc_waves = 0;
-            }
-#endif
-#if RT_TIMING
             TM_ADD(2, TM_NOW() - tm_start);
-            if (!GEN) {
-                TM_ADD(0, tq_regen);
-                TM_ADD(1, tq_norm);
-                TM_ADD(3, tq_closest);
-                TM_ADD(4, tq_shade);
-                TM_ADD(5, tq_seg);
-            }
-            if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
-                __threadfence();
-                printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
-                       "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu | passes_time %llu passes %llu\n",
-                       g_tm[0], g_tm[1], g_tm[2], g_tm[3], g_tm[4], g_tm[5], g_tm[6], g_tm[7], g_tm[8], g_tm[9],
-                       g_tm[10], g_tm[11], g_tm[12], g_tm[13]);
-                for (int i = 0; i < 16; ++i) g_tm[i] = 0;
-                g_tm_waves = 0;
-            }
-#endif
+            DIAG_WAVE_EXIT(GEN);
             break;
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
-#if RT_TIMING
-        bool fin = false;
-        if (GEN) {
-            fin = segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have;
-        } else {
-            tq_seg += 1;
-            const unsigned long long t0 = TM_NOW();
-            if (have) p.ray.d = normalize(p.ray.d);
-            const unsigned long long t1 = TM_NOW();
-            Hit h;
-            bool hit = false;
-            if (have) hit = closest<false, GEN, RESTART>(sc, p.ray, &h, st, c);
-            const unsigned long long t2 = TM_NOW();
-            if (have) fin = shade<false, GEN, DLS>(sc, p, h, hit, c);
-            const unsigned long long t3 = TM_NOW();
-            tq_norm += t1 - t0;
-            tq_closest += t2 - t1;
-            tq_shade += t3 - t2;
-        }
-#else
         const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
-#endif
         if (fin) {
             if (GEN) VC(13, 1);
             float* r = a.radiance + 3 * (size_t)slot;

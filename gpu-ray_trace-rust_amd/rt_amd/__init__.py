@@ -11,17 +11,6 @@ import os
 # and is kept (the library then sizes its pipeline to it; bench.py and lib/rt_render choose 16
 # themselves).  hw_queues() reports the value HIP started with, as far as this process can tell.
 RECOMMENDED_HW_QUEUES = 16
-_SET_BY_RT_AMD = "GPU_MAX_HW_QUEUES" not in os.environ
-if _SET_BY_RT_AMD:
-    os.environ["GPU_MAX_HW_QUEUES"] = str(RECOMMENDED_HW_QUEUES)
-
-
-def hw_queues() -> dict:
-    """{"value": GPU_MAX_HW_QUEUES as set, "source": "rt_amd" | "caller",
-    "hip_started_before_import": bool | None} — with HIP already started when rt_amd was first
-    imported the variable had no effect (HIP's default of 4 queues then applies)."""
-    return {"value": os.environ.get("GPU_MAX_HW_QUEUES"), "source": "rt_amd" if _SET_BY_RT_AMD else "caller",
-            "hip_started_before_import": _HIP_STARTED_BEFORE}
 
 
 def _hip_started() -> bool | None:
@@ -36,12 +25,27 @@ def _hip_started() -> bool | None:
         return None
 
 
+# Written only while HIP has not started: once it has, the queues are fixed, and a value written
+# now would make the library size its pipeline for queues HIP never created (it reads the variable
+# at rt_create as "what HIP started with").  Unset, the library assumes HIP's default of 4.
 _HIP_STARTED_BEFORE = _hip_started()
-if _HIP_STARTED_BEFORE:
+_SET_BY_RT_AMD = "GPU_MAX_HW_QUEUES" not in os.environ and _HIP_STARTED_BEFORE is False
+if _SET_BY_RT_AMD:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(RECOMMENDED_HW_QUEUES)
+if _HIP_STARTED_BEFORE and "GPU_MAX_HW_QUEUES" not in os.environ:
     import warnings
 
-    warnings.warn("rt_amd imported after HIP started: GPU_MAX_HW_QUEUES has no effect, the launch "
-                  "pipeline may share hardware queues (import rt_amd before using the GPU)")
+    warnings.warn("rt_amd imported after HIP started: HIP runs with its default of 4 hardware queues, so "
+                  "small batches overlap less (import rt_amd, or set GPU_MAX_HW_QUEUES, before using the GPU)")
+
+
+def hw_queues() -> dict:
+    """{"value": GPU_MAX_HW_QUEUES as set (None: HIP's default of 4), "source": "rt_amd" | "caller" |
+    None, "hip_started_before_import": bool | None}."""
+    v = os.environ.get("GPU_MAX_HW_QUEUES")
+    return {"value": v, "source": "rt_amd" if _SET_BY_RT_AMD else ("caller" if v is not None else None),
+            "hip_started_before_import": _HIP_STARTED_BEFORE}
+
 
 from . import abi  # noqa: E402,F401
 from .abi import load_library, RtError  # noqa: E402,F401

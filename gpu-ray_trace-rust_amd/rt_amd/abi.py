@@ -141,6 +141,8 @@ EXPORTS = {
                                    C.c_void_p]),
     "rt_render_device_async": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
+    "rt_render_batches_device_async": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64,
+                                                 C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p), C.c_void_p]),
     "rt_render_range": (C.c_int, [C.c_void_p, C.POINTER(rt_tile), C.c_uint32, C.c_uint64, C.c_uint32, P_f]),
     "rt_synchronize": (C.c_int, [C.c_void_p]),
     "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P_f]),

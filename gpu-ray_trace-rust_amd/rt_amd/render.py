@@ -147,6 +147,18 @@ class Context:
                                                             C.c_void_p(dev_ptr), C.c_void_p(stream or None)),
                   self.ctx)
 
+    def render_batches_device_async(self, dev_ptrs, tiles=None, sample_begin: int = 0, batch: int = 1,
+                                    stream: int = 0):
+        """render_to_target_gpu's batch loop on the device (rt_render_batches_device_async):
+        len(dev_ptrs) batches of `batch` samples from sample_begin, batch k's frame into
+        dev_ptrs[k] (0: not written).  Enqueued on `stream` like render_device_async."""
+        tiles = tiles or self.full_tile()
+        arr, n = tiles_array(tiles)
+        outs = (C.c_void_p * len(dev_ptrs))(*[C.c_void_p(p or None) for p in dev_ptrs])
+        abi.check(self.lib, self.lib.rt_render_batches_device_async(
+            self.ctx, arr, n, int(sample_begin), int(batch), len(dev_ptrs), outs, C.c_void_p(stream or None)),
+            self.ctx)
+
     def synchronize(self):
         abi.check(self.lib, self.lib.rt_synchronize(self.ctx), self.ctx)
 

@@ -82,38 +82,57 @@ def step_samples(width: int, height: int, spp: int, world: int, strong: bool) ->
     return spp_rank, width * height * spp_rank
 
 
+GATHER_MODES = ("frame", "step")
+
+
+def gather_steps(steps: int, mode: str) -> list:
+    """Which of a run's `steps` steps end in the gather: "frame" (north_star's single gather of
+    tile radiance at frame end) only the last one; "step" (the reference's per-batch read-back,
+    draw_scene.rs:34-42) every one."""
+    if mode not in GATHER_MODES:
+        raise ValueError(f"gather mode {mode!r}: one of {GATHER_MODES}")
+    return [mode == "step" or i == steps - 1 for i in range(steps)]
+
+
 class FrameSteps:
     """The step loop of a sharded frame, as bench.py times it and the multi-rank
     tests run it: each step renders `spp_rank` more samples of this rank's stripes into one device
-    buffer (rt_render_device_async on torch's current stream, or the synchronous rt_render_device),
-    then gathers every rank's buffer to rank 0 — the one collective per step.  backend "nccl"
-    (RCCL over xGMI) gathers the device buffers on torch's stream behind the step's fold; "gloo"
-    gathers host copies (several ranks sharing one GPU, where RCCL refuses)."""
+    buffer (rt_render_device_async on torch's current stream, or the synchronous rt_render_device);
+    the gather of every rank's buffer to rank 0 — the one collective — runs after the last step of
+    the frame (gather="frame") or after every step (gather="step").  backend "nccl" (RCCL over
+    xGMI) gathers the device buffers on torch's stream behind the step's fold; "gloo" gathers host
+    copies (several ranks sharing one GPU, where RCCL refuses)."""
 
     def __init__(self, ctx, tiles, width: int, height: int, rank: int, world: int, stripe: int,
-                 spp_rank: int, device: int, dist=None, backend: str = "nccl", sync: bool = False):
+                 spp_rank: int, device: int, dist=None, backend: str = "nccl", sync: bool = False,
+                 gather: str = "frame"):
         import torch
 
         self.torch = torch
         self.ctx, self.tiles = ctx, tiles
         self.width, self.height, self.rank, self.world, self.stripe = width, height, rank, world, stripe
         self.spp_rank, self.dist, self.backend, self.sync = spp_rank, dist, backend, sync
+        gather_steps(1, gather)  # validates the mode
+        self.gather_mode = gather
+        self.n_gathers = 0
         self.npix = tile_pixels(tiles)
         n = max(max_rank_pixels(width, height, world, stripe), self.npix)
-        self.out = torch.zeros((n, 4), dtype=torch.float32, device=f"cuda:{device}")
+        # device None: host buffers and no HIP at all (the CPU tests' stand-in context)
+        self.on_cpu = device is None
+        self.out = torch.zeros((n, 4), dtype=torch.float32, device="cpu" if self.on_cpu else f"cuda:{device}")
         self.device = device
-        on_host = backend == "gloo"
+        on_host = backend == "gloo" or self.on_cpu
         self.gather = None
         if dist is not None and rank == 0:
             self.gather = [torch.empty((n, 4), dtype=torch.float32, device="cpu" if on_host else f"cuda:{device}")
                            for _ in range(world)]
-        self.stream = torch.cuda.current_stream().cuda_stream
+        self.stream = 0 if self.on_cpu else torch.cuda.current_stream().cuda_stream
         self.sample = 0
         self.gather_ev = []
         self.gather_s = []
         self.sync_stats = []
 
-    def step(self):
+    def step(self, gather: bool = True):
         torch = self.torch
         if self.sync:
             self.ctx.render_device(self.out.data_ptr(), self.tiles, self.sample, self.spp_rank)
@@ -122,8 +141,9 @@ class FrameSteps:
             self.ctx.render_device_async(self.out.data_ptr(), self.tiles, self.sample, self.spp_rank,
                                          stream=self.stream)
         self.sample += self.spp_rank
-        if self.dist is None:
+        if self.dist is None or not gather:
             return
+        self.n_gathers += 1
         if self.backend == "gloo":
             import time
 
@@ -141,7 +161,8 @@ class FrameSteps:
     def barrier(self):
         if self.dist is not None:
             self.dist.barrier()
-        self.torch.cuda.synchronize()
+        if not self.on_cpu:
+            self.torch.cuda.synchronize()
 
     def run(self, steps: int, warmup: int) -> dict:
         """W untimed steps, then exactly `steps` steps between barrier + synchronize on both
@@ -149,33 +170,53 @@ class FrameSteps:
         the timed steps, gather_ms_per_step}."""
         import time
 
-        for _ in range(warmup):
-            self.step()
+        for g in gather_steps(warmup, self.gather_mode) if warmup else []:
+            self.step(gather=g)
         self.ctx.synchronize()
         self.barrier()
         self.gather_ev.clear()
         self.gather_s.clear()
         self.sync_stats.clear()
+        self.n_gathers = 0
         t0 = time.perf_counter()
-        for _ in range(steps):
-            self.step()
+        for g in gather_steps(steps, self.gather_mode):
+            self.step(gather=g)
         self.ctx.synchronize()
         self.barrier()
         elapsed = time.perf_counter() - t0
+        # the final result on the host (SURVEY.md §8d): one D2H copy of the frame after the timed
+        # steps, timed on its own (rank 0: the gathered buffers; every rank waits for it)
+        t1 = time.perf_counter()
+        if self.rank == 0:
+            parts = self.gather if self.dist is not None else [self.out]
+            self.host_frame_parts = [p.cpu() for p in parts]
+        self.barrier()
+        host_copy = time.perf_counter() - t1
         if self.sync:
             ls = {k: sum(s[k] for s in self.sync_stats)
                   for k in ("render_ms", "trace_ms", "n_trace_launches", "n_timed_launches")}
         else:
             ls = self.ctx.launch_stats()
         if self.dist is not None:
-            t = self.torch.tensor([elapsed], device="cpu" if self.backend == "gloo" else f"cuda:{self.device}")
+            t = self.torch.tensor([elapsed], device="cpu" if self.backend == "gloo" or self.on_cpu else f"cuda:{self.device}")
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        res = {"elapsed_s": elapsed, "launch": ls}
+        if self.dist is not None:
+            t = self.torch.tensor([host_copy], device="cpu" if self.backend == "gloo" or self.on_cpu else f"cuda:{self.device}")
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            host_copy = float(t.item())
+        res = {"elapsed_s": elapsed, "launch": ls, "host_copy_s": host_copy, "gathers": self.n_gathers,
+               "gather_mode": self.gather_mode}
+        # gather time: per gather, and spread over the run's steps (one gather per frame: / steps)
         if self.gather_ev:
-            res["gather_ms_per_step"] = sum(a.elapsed_time(b) for a, b in self.gather_ev) / len(self.gather_ev)
+            tot = sum(a.elapsed_time(b) for a, b in self.gather_ev)
         elif self.gather_s:
-            res["gather_ms_per_step"] = 1e3 * sum(self.gather_s) / len(self.gather_s)
+            tot = 1e3 * sum(self.gather_s)
+        else:
+            tot = None
+        if tot is not None:
+            n = len(self.gather_ev) or len(self.gather_s)
+            res.update(gather_ms_per_gather=tot / n, gather_ms_per_step=tot / steps)
         return res
 
     def frame(self):
@@ -183,6 +224,6 @@ class FrameSteps:
         a host array (the single-rank frame for world 1); None elsewhere."""
         if self.rank != 0:
             return None
-        parts = self.gather if self.dist is not None else [self.out]
+        parts = getattr(self, "host_frame_parts", None) or (self.gather if self.dist is not None else [self.out])
         f = assemble(parts, self.width, self.height, self.world, self.stripe)
         return f.cpu().numpy() if hasattr(f, "cpu") else f

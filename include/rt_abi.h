@@ -257,6 +257,18 @@ int rt_render_device_async(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
                            uint64_t sample_begin, uint32_t sample_count, float* out_rgba_device,
                            void* stream);
 
+/* The batch loop of render_to_target_gpu (draw_scene.rs:30-44) on the device, asynchronous like
+ * rt_render_device_async: n_batches consecutive batches of `batch` samples from sample_begin;
+ * after batch k the running mean over [0, sample_begin + (k + 1) * batch) is written to
+ * outs_dev[k] (device memory; NULL: that frame is not written, the accumulator still advances).
+ * The frames equal n_batches rt_render_device_async calls bit for bit.  The batches are traced by
+ * as few launches as the radiance buffer allows and folded batch by batch, so small batches (a
+ * 1-spp batch of a 1200x600 frame) keep the GPU busy without one pipeline stream, and HIP
+ * hardware queue, per batch in flight (GPU_MAX_HW_QUEUES does not matter). */
+int rt_render_batches_device_async(rt_ctx* ctx, const rt_tile* tiles, uint32_t n_tiles,
+                                   uint64_t sample_begin, uint32_t batch, uint32_t n_batches,
+                                   float* const* outs_dev, void* stream);
+
 /* The mean over samples [sample_begin, sample_begin + sample_count) alone, per pixel of `tiles`
  * (RGBA f32, alpha 1, tiles concatenated): what one batch of the reference's GPU path returns
  * (block_and_get_single_result, gpu_utils.rs:681-724, whose kernel folds the batch with a

@@ -1,0 +1,98 @@
+// stub_hip.cpp — a host-only stand-in for the HIP runtime entry points librt_amd.so imports, for
+// CPU tests of the runtime's host logic (tests/test_runtime_stub.py).  LD_PRELOADed, it answers
+// every call the library makes: one "gfx950" device, host memory for device allocations, streams
+// and events as tokens, kernel launches counted and not run.  hipEventQuery answers what
+// stub_hip_set_query() chose, so a test can make the launch pipeline see a failed earlier launch.
+// Test infrastructure only: never on the GPU box, never linked into the product.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdlib>
+#include <cstring>
+
+namespace {
+thread_local hipError_t g_last = hipSuccess;
+hipError_t g_query = hipSuccess;
+int g_launches = 0;
+int g_log[4096];  // block size of every launch, in order (128: a trace kernel, 256: the fold)
+int g_tokens[1024];
+int g_next_token = 0;
+dim3 g_grid, g_block;
+size_t g_shmem = 0;
+hipStream_t g_stream = nullptr;
+
+hipError_t ret(hipError_t e) {
+    if (e != hipSuccess) g_last = e;
+    return e;
+}
+void* token() { return &g_tokens[(g_next_token++) & 1023]; }
+}  // namespace
+
+extern "C" {
+// test controls
+void stub_hip_set_query(int e) { g_query = static_cast<hipError_t>(e); }
+int stub_hip_launches(void) { return g_launches; }
+int stub_hip_launch_log(int* out, int n) {
+    const int m = g_launches < 4096 ? g_launches : 4096;
+    for (int i = 0; i < m && i < n; ++i) out[i] = g_log[i];
+    return m;
+}
+
+hipError_t hipGetDeviceCount(int* n) { *n = 1; return hipSuccess; }
+hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_t* p, int dev) {
+    if (dev != 0) return ret(hipErrorInvalidDevice);
+    std::memset(p, 0, sizeof(*p));
+    std::strcpy(p->name, "stub");
+    std::strcpy(p->gcnArchName, "gfx950:sramecc+:xnack-");
+    p->multiProcessorCount = 256;
+    return hipSuccess;
+}
+hipError_t hipSetDevice(int) { return hipSuccess; }
+hipError_t hipMalloc(void** p, size_t n) {
+    *p = std::calloc(1, n ? n : 1);
+    return *p ? hipSuccess : ret(hipErrorOutOfMemory);
+}
+hipError_t hipFree(void* p) { std::free(p); return hipSuccess; }
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) { std::memcpy(d, s, n); return hipSuccess; }
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+    std::memcpy(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemset(void* d, int v, size_t n) { std::memset(d, v, n); return hipSuccess; }
+hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) { std::memset(d, v, n); return hipSuccess; }
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = static_cast<hipStream_t>(token()); return hipSuccess; }
+hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
+hipError_t hipEventCreate(hipEvent_t* e) { *e = static_cast<hipEvent_t>(token()); return hipSuccess; }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { *e = static_cast<hipEvent_t>(token()); return hipSuccess; }
+hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) { *ms = 1.0f; return hipSuccess; }
+hipError_t hipEventQuery(hipEvent_t) { return ret(g_query); }
+hipError_t hipGetLastError(void) {
+    const hipError_t e = g_last;
+    g_last = hipSuccess;
+    return e;
+}
+const char* hipGetErrorString(hipError_t e) {
+    return e == hipErrorLaunchFailure ? "stub: unspecified launch failure" : "stub error";
+}
+hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, const void*, int, size_t) { *n = 16; return hipSuccess; }
+hipError_t hipLaunchKernel(const void*, dim3, dim3 block, void**, size_t, hipStream_t) {
+    if (g_launches < 4096) g_log[g_launches] = (int)block.x;
+    ++g_launches;
+    return hipSuccess;
+}
+hipError_t __hipPushCallConfiguration(dim3 grid, dim3 block, size_t shmem, hipStream_t s) {
+    g_grid = grid, g_block = block, g_shmem = shmem, g_stream = s;
+    return hipSuccess;
+}
+hipError_t __hipPopCallConfiguration(dim3* grid, dim3* block, size_t* shmem, hipStream_t* s) {
+    *grid = g_grid, *block = g_block, *shmem = g_shmem, *s = g_stream;
+    return hipSuccess;
+}
+void** __hipRegisterFatBinary(const void*) { return reinterpret_cast<void**>(token()); }
+void __hipRegisterFunction(void**, const void*, char*, const char*, unsigned, void*, void*, void*, void*, int*) {}
+void __hipUnregisterFatBinary(void**) {}
+}

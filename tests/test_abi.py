@@ -137,6 +137,28 @@ def test_hw_queues_report():
     assert r == {"value": "16", "source": "rt_amd", "hip_started_before_import": False}
 
 
+def test_hw_queues_untouched_after_hip_started():
+    """With HIP already started (here a stand-in torch whose cuda.is_initialized() is True) the
+    queues are fixed: rt_amd must not write GPU_MAX_HW_QUEUES, or the library would size its
+    pipeline for 16 queues HIP never made.  It stays unset, the library then assumes
+    HIP's default of 4, and hw_queues() says HIP had started."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    code = ("import os, sys, types, json, warnings; warnings.simplefilter('ignore'); "
+            "t = types.ModuleType('torch'); t.cuda = types.SimpleNamespace(is_initialized=lambda: True); "
+            "sys.modules['torch'] = t; sys.path.insert(0, %r); import rt_amd; "
+            "print(json.dumps([os.environ.get('GPU_MAX_HW_QUEUES'), rt_amd.hw_queues()]))"
+            % os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    v, r = json.loads(out.stdout)
+    assert v is None
+    assert r == {"value": None, "source": None, "hip_started_before_import": True}
+
+
 def test_committed_counters_belong_to_this_build():
     """bench.py prices each config's roofline with the committed rocprofv3 counters of the SAME
     device code (profiles/*_counters.json, keyed on the .hip_fatbin hash): every bench config's

@@ -90,3 +90,20 @@ int main(void) {
     subprocess.run(["gcc", "-O0", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout
+
+
+def test_shipped_library_has_no_device_printf():
+    """The diagnostic instrumentation (csrc/kernel/diag.h: clock reads, counters, printf) is
+    compiled only into `make diag`'s libraries.  A device printf makes the kernel take the
+    hostcall buffer (metadata `hidden_hostcall_buffer`); the shipped code object must have none.
+    When the diagnostic libraries are built, they are checked to carry it, so the probe can see
+    a printf when there is one."""
+    import os
+
+    from rt_amd import abi
+
+    assert b"hostcall" not in _gfx950_object(abi.LIB_PATH)
+    assert b"printf" not in _gfx950_object(abi.LIB_PATH)
+    diag = os.path.join(os.path.dirname(abi.LIB_PATH), "variants", "librt_diag_timing.so")
+    if os.path.exists(diag):
+        assert b"hostcall" in _gfx950_object(diag)

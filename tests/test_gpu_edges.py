@@ -125,15 +125,15 @@ def test_empty_leaves_with_stale_offsets(gpu_available, monkeypatch):
     t = tree.as_struct(nodes=nodes)
     imgs = {}
     for cfg in (("1", "0"), ("0", "0"), ("1", "1")):
-        monkeypatch.setenv("RT_PACKET", cfg[0])
-        monkeypatch.setenv("RT_KD_RESTART", cfg[1])
+        monkeypatch.setenv("RT_DEBUG_PACKET", cfg[0])
+        monkeypatch.setenv("RT_DEBUG_KD_RESTART", cfg[1])
         with render.Context(sc, tree=t) as c:
             imgs[cfg] = c.render(None, 0, 2)
     ref = imgs[("1", "0")]
     for cfg, g in imgs.items():
         assert np.array_equal(g, ref), (cfg, parity.stats(g, ref))
-    monkeypatch.setenv("RT_PACKET", "1")
-    monkeypatch.setenv("RT_KD_RESTART", "0")
+    monkeypatch.setenv("RT_DEBUG_PACKET", "1")
+    monkeypatch.setenv("RT_DEBUG_KD_RESTART", "0")
     with render.Context(sc) as c:
         full = c.render(None, 0, 2)
     assert not np.array_equal(full, ref)

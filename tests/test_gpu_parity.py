@@ -167,10 +167,10 @@ def test_dir_light_samp_schedules_agree(gpu_available, monkeypatch):
     sc = load_scene("walled")
     sc.info.dir_light_samp = 1
     tiles = [(560, 260, 40, 20), (3, 5, 9, 7)]
-    monkeypatch.setenv("RT_SCHED", "direct")
+    monkeypatch.setenv("RT_DEBUG_SCHED", "direct")
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, 9)
-    monkeypatch.setenv("RT_SCHED", "queue")
+    monkeypatch.setenv("RT_DEBUG_SCHED", "queue")
     with render.Context(sc) as c2:
         assert np.array_equal(c2.render(tiles, 0, 9), ref)
 
@@ -182,11 +182,11 @@ def test_lanes_per_pixel_bit_invariant(gpu_available, walled, monkeypatch, k, sp
     from rt_amd import render
 
     crops = CROPS[:2] if spp < 100 else [(560, 260, 16, 8)]
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", "1")
+    monkeypatch.setenv("RT_DEBUG_LANES_PER_PIXEL", "1")
     with render.Context(walled) as c1:
         ref = c1.render(crops, 0, spp)
         ref2 = c1.render(crops, spp, 5)
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", str(k))
+    monkeypatch.setenv("RT_DEBUG_LANES_PER_PIXEL", str(k))
     with render.Context(walled) as ck:
         g = ck.render(crops, 0, spp)
         g2 = ck.render(crops, spp, 5)
@@ -213,11 +213,11 @@ def test_queue_schedule_bit_invariant(gpu_available, monkeypatch, scene_name, sp
     sc = load_scene(scene_name)
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 40, h // 2 - 20, 80, 40), (0, 0, 7, 3), (w - 33, h - 9, 33, 9)]
-    monkeypatch.setenv("RT_SCHED", "direct")
+    monkeypatch.setenv("RT_DEBUG_SCHED", "direct")
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, spp)
         ref2 = c1.render(tiles, spp, 4)
-    monkeypatch.setenv("RT_SCHED", "queue")
+    monkeypatch.setenv("RT_DEBUG_SCHED", "queue")
     with render.Context(sc) as cq:
         g = cq.render(tiles, 0, spp)
         g2 = cq.render(tiles, spp, 4)
@@ -236,10 +236,10 @@ def test_split_queue_launches_bit_invariant(gpu_available, monkeypatch, scene_na
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 40, h // 2 - 20, 80, 40), (w - 33, h - 9, 33, 9)]
     n_pix = 80 * 40 + 33 * 9
-    monkeypatch.delenv("RT_QUEUE_RADIANCE_FLOATS", raising=False)
+    monkeypatch.delenv("RT_DEBUG_RADIANCE_FLOATS", raising=False)
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, spp)
-    monkeypatch.setenv("RT_QUEUE_RADIANCE_FLOATS", str(3 * n_pix * 4))  # 4 samples per launch
+    monkeypatch.setenv("RT_DEBUG_RADIANCE_FLOATS", str(3 * n_pix * 4))  # 4 samples per launch
     with render.Context(sc) as cs:
         g = cs.render(tiles, 0, spp)
         n_split = cs.launch_stats()["n_trace_launches"]
@@ -379,11 +379,11 @@ def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, sp
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, spp)
     for pipe, cap in (("2", None), ("0", None), ("2", str(3 * n * 2))):  # cap: 2 samples per launch
-        monkeypatch.setenv("RT_PIPELINE", pipe)  # overlapped launches, or each after the last fold
+        monkeypatch.setenv("RT_DEBUG_PIPELINE", pipe)  # overlapped launches, or each after the last fold
         if cap:
-            monkeypatch.setenv("RT_QUEUE_RADIANCE_FLOATS", cap)
+            monkeypatch.setenv("RT_DEBUG_RADIANCE_FLOATS", cap)
         else:
-            monkeypatch.delenv("RT_QUEUE_RADIANCE_FLOATS", raising=False)
+            monkeypatch.delenv("RT_DEBUG_RADIANCE_FLOATS", raising=False)
         with render.Context(sc) as ca:
             out = torch.full((n, 4), -1.0, dtype=torch.float32, device="cuda:0")
             stream = torch.cuda.current_stream().cuda_stream
@@ -396,8 +396,8 @@ def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, sp
         assert np.array_equal(got, ref), (pipe, cap, parity.stats(got, ref))
     # a synchronous call between async ones
     assert spp >= 3 * batch
-    monkeypatch.delenv("RT_QUEUE_RADIANCE_FLOATS", raising=False)
-    monkeypatch.delenv("RT_PIPELINE", raising=False)
+    monkeypatch.delenv("RT_DEBUG_RADIANCE_FLOATS", raising=False)
+    monkeypatch.delenv("RT_DEBUG_PIPELINE", raising=False)
     with render.Context(sc) as cm:
         out = torch.zeros((n, 4), dtype=torch.float32, device="cuda:0")
         cm.render_device_async(out.data_ptr(), tiles, 0, batch)
@@ -433,9 +433,9 @@ def test_render_to_target_pipelined_equals_batches(gpu_available, scene_name, sp
 @pytest.mark.parametrize("scene_name,spp", [("walled", 9), ("triangles", 4), ("biplane", 3), ("spaceship_r1", 3),
                                             ("a380", 2)])
 def test_stackless_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scene_name, spp):
-    """Stackless kd-restart with push-down (RT_KD_RESTART=1: after a leaf, descend again from the
+    """Stackless kd-restart with push-down (RT_DEBUG_KD_RESTART=1: after a leaf, descend again from the
     deepest node above the first push, entry = the leaf's exit) and the stackless kernel with the
-    leaves' triangles staged in LDS (RT_KD_RESTART=2) each render the forward oracle's image (the
+    leaves' triangles staged in LDS (RT_DEBUG_KD_RESTART=2) each render the forward oracle's image (the
     reference's stack traversal, kdtree.rs:66-104), bit for bit, in the queue kernels."""
     from rt_amd import render
 
@@ -444,7 +444,7 @@ def test_stackless_traversal_bit_invariant(gpu_available, oracle, monkeypatch, s
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
     o = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
     for rs in ("0", "1", "2"):
-        monkeypatch.setenv("RT_KD_RESTART", rs)
+        monkeypatch.setenv("RT_DEBUG_KD_RESTART", rs)
         with render.Context(sc) as c:
             g = c.render(tiles, 0, spp)
         assert np.array_equal(g, o), (rs, parity.stats(g, o))
@@ -455,7 +455,7 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
     """Camera-ray packets (closest_packet: scalar-loaded nodes and leaf refs, per-lane
     near / far / push on the lane's own interval, deferred lanes, kd-restart from the packet's
     restart node, hand-over to the cooperative search), the cooperative search alone
-    (RT_PACKET=0) and the row-order queue (RT_PIX_BLOCK=1) each render the forward oracle's image
+    (RT_DEBUG_PACKET=0) and the row-order queue (RT_DEBUG_PIX_BLOCK=1) each render the forward oracle's image
     (kdtree.rs:66-104), bit for bit, on two tiles and a full frame."""
     from rt_amd import render
 
@@ -465,8 +465,8 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
     o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
     o_full = oracle.render(sc, [(0, 0, w, h)], 0, 2 * spp, accum=oracle.ACCUM_FORWARD)
     for cfg in (("1", "8"), ("0", "1"), ("1", "1"), ("0", "8")):
-        monkeypatch.setenv("RT_PACKET", cfg[0])
-        monkeypatch.setenv("RT_PIX_BLOCK", cfg[1])
+        monkeypatch.setenv("RT_DEBUG_PACKET", cfg[0])
+        monkeypatch.setenv("RT_DEBUG_PIX_BLOCK", cfg[1])
         with render.Context(sc) as c:
             got = c.render(tiles, 0, spp)
         assert np.array_equal(got, o_tiles), (cfg, parity.stats(got, o_tiles))
@@ -490,7 +490,7 @@ def test_queue_shards_bit_invariant(gpu_available, oracle, monkeypatch, scene_na
     o_full = oracle.render(sc, [(0, 0, w, h)], 0, spp, accum=oracle.ACCUM_FORWARD)
     o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
     for n in ("1", "3", "8", "32"):
-        monkeypatch.setenv("RT_QUEUE_SHARDS", n)
+        monkeypatch.setenv("RT_DEBUG_QUEUE_SHARDS", n)
         with render.Context(sc) as c:
             full = c.render(None, 0, spp)
             got = c.render(tiles, 0, spp)
@@ -512,8 +512,8 @@ def test_small_launch_pipeline_bit_invariant(gpu_available, oracle, monkeypatch)
     spp = 6
     o = oracle.render(sc, [(0, 0, w, h)], 0, spp, accum=oracle.ACCUM_FORWARD)
     for slots, div in (("12", "8"), ("12", "2"), ("3", "16")):
-        monkeypatch.setenv("RT_PIPELINE_SLOTS", slots)
-        monkeypatch.setenv("RT_QUEUE_GRID_DIV", div)
+        monkeypatch.setenv("RT_DEBUG_PIPELINE_SLOTS", slots)
+        monkeypatch.setenv("RT_DEBUG_GRID_DIV", div)
         with render.Context(sc) as c:
             out = torch.zeros((w * h, 4), dtype=torch.float32, device="cuda:0")
             stream = torch.cuda.current_stream().cuda_stream

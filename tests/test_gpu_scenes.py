@@ -74,13 +74,13 @@ def test_debug_single_ray_scene(scene, oracle):
 @pytest.mark.parametrize("name", ["triangles", "biplane", "spaceship_r1"])
 def test_texel_pool_u8_equals_f32(gpu_available, monkeypatch, name):
     """The 8-bit texel pool (every channel some k / 255: one RGBA8 word per texel, decoded on the
-    device) renders the f32 pool's image bit for bit (RT_TEXELS_F32=1 forces the f32 pool)."""
+    device) renders the f32 pool's image bit for bit (RT_DEBUG_TEXELS_F32=1 forces the f32 pool)."""
     from rt_amd import render
 
     sc = load_scene(name, width=320, height=160)
     with render.Context(sc) as c:
         g8 = c.render(None, 0, 3)
-    monkeypatch.setenv("RT_TEXELS_F32", "1")
+    monkeypatch.setenv("RT_DEBUG_TEXELS_F32", "1")
     with render.Context(sc) as c:
         g32 = c.render(None, 0, 3)
     assert np.array_equal(g8, g32), parity.stats(g8, g32)

@@ -81,9 +81,9 @@ def test_parallel_build_is_byte_identical(monkeypatch, name):
 
     sc = load_scene(name)
     depth = int(sc.info.kd_tree_depth)
-    monkeypatch.setenv("RT_KD_THREADS", "1")
+    monkeypatch.setenv("RT_DEBUG_KD_THREADS", "1")
     one = render.KdTree(sc.desc, depth)
-    monkeypatch.setenv("RT_KD_THREADS", "8")
+    monkeypatch.setenv("RT_DEBUG_KD_THREADS", "8")
     par = render.KdTree(sc.desc, depth)
     assert np.array_equal(one.nodes, par.nodes)
     assert np.array_equal(one.refs, par.refs)

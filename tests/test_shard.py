@@ -112,3 +112,82 @@ def test_step_sample_accounting(world):
         # and with equal stripe counts each rank's share is job / N (balanced)
         assert {shard.tile_pixels(shard.rank_tiles(w, h, r, world, stripe)) * spp_rank
                 for r in range(world)} == {job // world}
+
+
+@pytest.mark.parametrize("steps", [1, 3, 7])
+def test_gather_steps_pin_which_steps_gather(steps):
+    """"frame" (north_star's single gather at frame end): only the last step gathers; "step"
+    (the reference's per-batch read-back): every step does."""
+    from rt_amd import shard
+
+    assert shard.gather_steps(steps, "frame") == [False] * (steps - 1) + [True]
+    assert shard.gather_steps(steps, "step") == [True] * steps
+    with pytest.raises(ValueError):
+        shard.gather_steps(steps, "never")
+
+
+class _PatternCtx:
+    """Stand-in for render.Context on the CPU: writes, into the rank's host buffer, the value
+    every pixel of its tiles would hold after `sample_end` samples (pixel index, sample_end)."""
+
+    def __init__(self, w):
+        self.w, self.calls = w, []
+
+    def render_device_async(self, ptr, tiles, s0, n, stream=0):
+        import ctypes as C
+
+        from rt_amd import shard
+
+        npx = shard.tile_pixels(tiles)
+        buf = np.ctypeslib.as_array((C.c_float * (4 * npx)).from_address(ptr)).reshape(npx, 4)
+        off = 0
+        for (x0, y0, tw, th) in tiles:
+            ys, xs = np.mgrid[y0:y0 + th, x0:x0 + tw]
+            buf[off:off + tw * th, 0] = (ys * self.w + xs).ravel()
+            buf[off:off + tw * th, 1] = s0 + n
+            buf[off:off + tw * th, 3] = 1.0
+            off += tw * th
+        self.calls.append((s0, n))
+
+    def synchronize(self):
+        pass
+
+    def launch_stats(self):
+        return {"render_ms": 0.0, "trace_ms": 0.0, "n_trace_launches": len(self.calls), "n_timed_launches": 0}
+
+
+def _frame_steps_worker(rank, world, port, mode, res_path):
+    import torch.distributed as dist
+
+    from rt_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w, h, spp, steps = 40, 24, 3, 4
+        stripe = shard.stripe_rows(h, world)
+        tiles = shard.rank_tiles(w, h, rank, world, stripe)
+        fs = shard.FrameSteps(_PatternCtx(w), tiles, w, h, rank, world, stripe, spp, None, dist=dist,
+                              backend="gloo", gather=mode)
+        r = fs.run(steps, 2)
+        if rank == 0:
+            f = fs.frame()
+            ok = bool((f[..., 3] == 1).all() and (f[..., 1] == (2 + steps) * spp).all()
+                      and (f[..., 0] == np.arange(w * h).reshape(h, w)).all())
+            np.save(res_path, np.array([ok, r["gathers"], len(fs.ctx.calls)]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,gathers", [("frame", 1), ("step", 4)])
+def test_frame_steps_gathers_world2(tmp_path, mode, gathers):
+    """FrameSteps over gloo with two ranks (a CPU stand-in context): 4 timed steps after 2 warmup
+    ones; "frame" gathers once, after the last step, "step" after each; either way rank 0's frame
+    is every pixel after all 6 steps' samples."""
+    import torch.multiprocessing as mp
+
+    res = str(tmp_path / "r.npy")
+    mp.spawn(_frame_steps_worker, args=(2, _free_port(), mode, res), nprocs=2, join=True)
+    ok, n_gathers, calls = np.load(res)
+    assert ok and n_gathers == gathers and calls == 6

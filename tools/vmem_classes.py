@@ -1,5 +1,5 @@
 """Vector-memory load instructions of the general queue kernel by class, per sample (the
-RT_VMEM_COUNT diagnostic build: tools/build_variants.sh vmemcount="-DRT_VMEM_COUNT=1").
+RT_VMEM_COUNT diagnostic build: make -C gpu-ray_trace-rust_amd diag -> lib/variants/librt_diag_vmem.so).
 Renders one full-frame launch of each scene in a child process (the kernel's printf goes to the
 child's stdout) and prints one JSON line per scene: wave-level load instructions per sample by
 class, next to SQ_INSTS_VMEM_RD per sample from the committed counters of the product build.
@@ -20,7 +20,7 @@ import os, sys
 sys.path.insert(0, os.path.join(%(root)r, "gpu-ray_trace-rust_amd"))
 import torch  # noqa: F401
 from rt_amd import abi, render, scheme
-lib = abi.load_library(os.path.join(%(root)r, "gpu-ray_trace-rust_amd", "lib", "variants", "librt_vmemcount.so"))
+lib = abi.load_library(os.path.join(%(root)r, "gpu-ray_trace-rust_amd", "lib", "variants", "librt_diag_vmem.so"))
 sch = scheme.load_json(os.path.join(%(root)r, "tests", "golden", "scenes", %(scene)r + ".json"))
 loaded = scheme.load(sch, assets_root=os.path.join(%(root)r, "assets_pack"), lib=lib)
 with render.Context(loaded, lib=lib) as c:
@@ -36,7 +36,7 @@ def main(specs):
         spp = int(spp or 10)
         code = CHILD % {"root": ROOT, "scene": scene, "spp": spp}
         # serialized launches: the counters are per launch (overlapped launches would mix them)
-        env = dict(os.environ, RT_PIPELINE="0")
+        env = dict(os.environ, RT_DEBUG_PIPELINE="0")
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, env=env)
         # one "RT_VC <class> <count>" line per class and launch; the second launch's (the last 24)
         vc = [l.split() for l in r.stdout.splitlines() if l.startswith("RT_VC ")]
