@@ -76,8 +76,10 @@ static inline M3 mul(const M3& a, const M3& b) {
 static thread_local rt_rng_state g_rng;
 // Shading-mix instrumentation (counted renders only, tools/min_insts.py): per continued ray by
 // branch, the draws, and the Russian-roulette draws.
+// MIX_NODE_D0 + d: branch nodes the traversal steps through at depth d (root = 0), the
+// counted renders' descent profile (how much of a descent a top-of-tree node cache could hold)
 enum { MIX_SPEC, MIX_DIFF, MIX_DIFFSPEC_DIFF, MIX_DIFFSPEC_SPEC, MIX_DIELECTRIC, MIX_RR, MIX_DRAWS, MIX_MESH,
-       MIX_POSDISC, MIX_N };
+       MIX_POSDISC, MIX_NODE_D0, MIX_N = MIX_NODE_D0 + 40 };
 static thread_local uint64_t* g_mix = nullptr;
 #define MIX(i) do { if (g_mix) g_mix[i]++; } while (0)
 static std::mutex g_mix_mu;
@@ -711,16 +713,18 @@ struct KdTree {
 
     // stack_search (kdtree.rs:66-104)
     Closest stack_search(const Ray& ray, float entry_t0, float exit_t0) const {
-        struct Item { const Node* n; float entry, exit; };
+        struct Item { const Node* n; float entry, exit; int depth; };  // depth: instrumentation only
         std::vector<Item> stack;
-        stack.push_back(Item{node.get(), entry_t0, exit_t0});
+        stack.push_back(Item{node.get(), entry_t0, exit_t0, 0});
         while (!stack.empty()) {
             Item it = stack.back();
             stack.pop_back();
             const Node* cur = it.n;
             float entry_t = it.entry, exit_t = it.exit;
+            int depth = it.depth;
             while (!cur->leaf) {
                 COUNT(nodes, 1);
+                if (g_mix) g_mix[MIX_NODE_D0 + (depth < 39 ? depth : 39)]++;
                 int a = cur->axis;
                 float d = ray.d[a];
                 if (std::fabs(d) < EPS) d = d < 0.0f ? -EPS : EPS;
@@ -732,10 +736,11 @@ struct KdTree {
                 } else if (t <= entry_t) {
                     cur = far;
                 } else {
-                    stack.push_back(Item{far, t, exit_t});
+                    stack.push_back(Item{far, t, exit_t, depth + 1});
                     cur = near;
                     exit_t = t;
                 }
+                ++depth;
             }
             COUNT(nodes, 1);
             COUNT(leaf_refs, cur->elems.size());
@@ -1150,8 +1155,8 @@ extern "C" void oracle_refract(const float d[3], const float n[3], float n_out, 
 // Shading mix of the counted renders since the last reset (continued rays by material branch:
 // spec, diff, diffspec->diff, diffspec->spec, dielectric; Russian-roulette draws; all draws;
 // mesh continues; forward-order segments' spheres with a positive discriminant), for
-// tools/min_insts.py.
-extern "C" void oracle_mix_counts(uint64_t out[9], int reset) {
+// tools/min_insts.py; then the traversal's branch-node visits by depth (tools/descent_depths.py).
+extern "C" void oracle_mix_counts(uint64_t out[MIX_N], int reset) {
     std::lock_guard<std::mutex> lk(g_mix_mu);
     for (int i = 0; i < MIX_N; ++i) {
         out[i] = g_mix_total[i];

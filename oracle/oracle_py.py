@@ -114,7 +114,7 @@ def mesh_normal_transforms(desc, n_tris):
 
 
 MIX_FIELDS = ("spec", "diff", "diffspec_diff", "diffspec_spec", "dielectric", "rr_draws", "draws", "mesh",
-              "sphere_disc_positive")
+              "sphere_disc_positive") + tuple(f"node_d{d}" for d in range(40))
 
 
 def mix_counts(reset=True):
