@@ -568,6 +568,17 @@ def main():
             "note": "SURVEY.md §8d canonical bytes of the REFERENCE algorithm's work (rt_count_work), priced "
                     "per launch over the launch's duration: not a roofline, the device skips most of this "
                     "work exactly (closest_small, DESIGN.md §5)"}
+        # north_star's ">= 40% of HBM-read roofline in the traversal loop": not a gate this kernel can be
+        # scored on, and the line says so
+        hbm = res["roofline"].get("hbm") or {}
+        res["north_star_hbm_gate"] = {
+            "reference_algorithm_GB_s": res["reference_work"]["GB_s"],
+            "reference_algorithm_frac_of_peak": round(res["reference_work"]["GB_s"] / HBM_PEAK_GBS, 2),
+            "measured_hbm_frac": hbm.get("frac"),
+            "scored": False,
+            "why": "the reference's traversal bytes at this rate would exceed the 8 TB/s peak (frac > 1): the "
+                   "device does not do that work (it skips it exactly), and what it does read hits L2/MALL, so HBM "
+                   "is a few percent busy; the kernel's measured limiter is `roofline.bound`"}
     ctx.close()
     single = rank == 0 and world == 1 and not args.as_rank
     if single and not args.no_cpu:

@@ -560,6 +560,11 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         if ((uint64_t)scene->n_spheres + scene->n_free_tris + n_mesh >= (1ull << 30))
             return set_err(c, RT_ERR_INVALID_ARG, "too many primitives");
         c->queue_shards = queue_shards(scene->n_spheres, scene->n_free_tris, n_mesh);
+        // A scene that small (triangles.yml: 6 primitives, ~24 us per item and lane) makes even a
+        // 7.2 M-sample launch mostly start-up and drain: its launches up to 2^24 samples go to the
+        // small-launch pipeline (round 3, tools/gpu_a380_calib.py, 10 spp per launch: 16,600
+        // Msamples/s on 2 slots with the full grid, 17,700-18,300 on 4-12 slots with a share).
+        if (c->queue_shards > 1) c->small_items = 1ull << 24;
         std::vector<float4> pool(3 * ((size_t)scene->n_spheres + scene->n_free_tris + n_mesh), make_float4(0.f, 0.f, 0.f, 0.f));
         for (uint32_t i = 0; i < scene->n_spheres; ++i) pool[3 * (size_t)i] = sph[i];
         std::memcpy(pool.data() + 3 * (size_t)scene->n_spheres, ftri.data(), ftri.size() * sizeof(float4));

@@ -23,6 +23,9 @@
 #ifndef RT_VMEM_COUNT
 #define RT_VMEM_COUNT 0
 #endif
+#ifndef RT_REGION_COUNT
+#define RT_REGION_COUNT 0
+#endif
 
 namespace rtd {
 
@@ -52,6 +55,45 @@ __device__ unsigned int g_vc_waves;
                            atomicAdd(&::rtd::g_vc[i], (unsigned long long)(n)); } while (0)
 #else
 #define VC(i, n) do { } while (0)
+#endif
+
+// RT_REGION_COUNT: wave-level executions of the sphere-only kernel's code regions (the first
+// active lane adds 1: one count per wave-instruction stream through the region) and, for RC_LANES,
+// the active lanes there — the dynamic side of the walled instruction accounting
+// (tools/walled_accounting.py: counts x the region's VALU instructions per execution in the
+// shipped ISA, reconciled with SQ_INSTS_VALU).  Regions: RC_* below.
+enum {
+    RC_ITER = 0,      // queue loop iterations with a path on some lane (= wave-segments)
+    RC_ITER_LANES,    // ... lanes with a path in them
+    RC_REGEN,         // path-start step taken (batched starts)
+    RC_BATCH,         // a batch of 64 camera rays made (make_start)
+    RC_ROOTS,         // closest_small: the roots of one sphere (some lane's ray line meets it)
+    RC_SLAB,          // closest_small: root slab test + in_return_leaf (some lane hit a sphere)
+    RC_FALLBACK,      // closest_small: the exact traversal below E (some lane not in the returning leaf)
+    RC_FB_NODES,      // ... its descent steps
+    RC_FB_LEAVES,     // ... its leaves
+    RC_SHADE_HIT,     // shade past the miss test (some lane hit)
+    RC_SEED,          // DiffSpec seed draw
+    RC_RR,            // Russian roulette draw (depth > assured_depth)
+    RC_SPEC,          // mirror continue
+    RC_DIELECTRIC,    // refraction continue
+    RC_DIFF,          // diffuse continue
+    RC_ATTEN_DIV,     // attenuated colour by division (p != 1)
+    RC_STORE,         // radiance stores (paths ending)
+    RC_CUBE,          // cube-map emission
+    RC_N = 24
+};
+#if RT_REGION_COUNT
+__device__ unsigned long long g_rc[RC_N];
+__device__ unsigned int g_rc_waves;
+#define RC(i) do { if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
+                        atomicAdd(&::rtd::g_rc[i], 1ull); } while (0)
+#define RC_LANES(i) do { const uint32_t n_ = (uint32_t)__popcll(__ballot(1)); \
+                         if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
+                             atomicAdd(&::rtd::g_rc[i], (unsigned long long)n_); } while (0)
+#else
+#define RC(i) do { } while (0)
+#define RC_LANES(i) do { } while (0)
 #endif
 
 #if RT_TIMING || RT_VMEM_COUNT
@@ -93,9 +135,17 @@ __device__ __forceinline__ void diag_round_sharing(uint32_t off, uint32_t cnt) {
 #endif
 
 // The last wave of a launch prints the launch's totals and clears them for the next launch.
-#if RT_TIMING || RT_VMEM_COUNT
+#if RT_TIMING || RT_VMEM_COUNT || RT_REGION_COUNT
 template <bool GEN>
 __device__ __forceinline__ void diag_wave_exit() {
+#if RT_REGION_COUNT
+    if (__lane_id() == 0 && atomicAdd(&g_rc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+        __threadfence();
+        for (int i = 0; i < RC_N; ++i) printf("RT_RC %d %llu\n", i, g_rc[i]);
+        for (int i = 0; i < RC_N; ++i) g_rc[i] = 0;
+        g_rc_waves = 0;
+    }
+#endif
 #if RT_VMEM_COUNT
     if (GEN && __lane_id() == 0 && atomicAdd(&g_vc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
         __threadfence();

@@ -226,6 +226,22 @@ __shared__ float4 g_lds_sph[RT_LDS_SPHERES];
 __shared__ float4 g_lds_csq[RT_LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
 __shared__ DevMat g_lds_mat[RT_LDS_SPHERES];
 __device__ __forceinline__ uint2 fetch_node(const DevScene& sc, uint32_t i) { return sc.nodes[i]; }
+// Experiment (RT_LDS_TOP = N > 0, off in the product): the first N nodes of
+// the blocked layout — the top of the tree (kd_build.cpp relayout_blocked: 128 nodes ~ 6 levels,
+// 1024 ~ 9) — copied into LDS per workgroup, and the cooperative descent and pops read those
+// nodes from LDS instead of through the vector-memory path.
+#ifndef RT_LDS_TOP
+#define RT_LDS_TOP 0
+#endif
+#if RT_LDS_TOP
+__shared__ uint2 g_top[RT_LDS_TOP];
+#endif
+__device__ __forceinline__ uint2 fetch_node_coop(const DevScene& sc, uint32_t i) {
+#if RT_LDS_TOP
+    if (i < (uint32_t)RT_LDS_TOP) return g_top[i];
+#endif
+    return sc.nodes[i];
+}
 // GEN == false (sphere-only kernel): spheres come from LDS.  The general kernel reads them from
 // global memory.
 template <bool GEN>
@@ -512,6 +528,7 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, c
         bool pushed = false;
         while ((nd.y & 3u) != RT_KD_LEAF) {
             if (COUNT) c.nodes++;
+            if (!GEN && SMALL) RC(RC_FB_NODES);
             float d;
             const float t = split_t<FAST>(nd, ax, r, &d);
             const bool pos = d > 0.0f;          // near = low when d > 0 (kdtree.rs:79)
@@ -532,6 +549,7 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, c
             nd = fetch_node(sc, node);
         }
         if (COUNT) { c.nodes++; c.leaf_refs += nd.x & LEAF_COUNT_MASK; }
+        if (!GEN && SMALL) RC(RC_FB_LEAVES);
         if (leaf_closest<COUNT, GEN, SMALL>(sc, nd.y >> 2, nd.x & LEAF_COUNT_MASK, r, best, c, imin, lmin) &&
             best->l <= exit_t + EPS)
             return true;
@@ -574,6 +592,16 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, c
 // (faces swap for d_a < 0) put S in leaf k whatever the tree.  t(face) is the traversal's
 // own arithmetic: the Markstein quotient with the ray's exact reciprocal, used only when
 // equal to the division (face - o in mk range); otherwise the traversal runs.
+//
+// The face distances are only compared, so the quotients need not be computed exactly: with
+// rc = RN(1 / d), q = RN(n * rc) lies within 2^-22 |q| of n / d (two roundings and rc's), so the
+// traversal's RN(n / d) lies in [q - |q| 2^-21, q + |q| 2^-21], and the test takes the bound on the
+// unfavourable side: t(near) <= E from q + |q| 2^-21 <= E, t(far) > L* from q - |q| 2^-21 > L*.
+// A true result is therefore true for the exact quotients; a marginal case just falls back to the
+// traversal.  (|n| < 2^61 and |rc| <= 1 / EPS: no overflow.  A product that underflows has
+// |q| < 2^-100 and an exact quotient as tiny: both are below E's floor ~1.7e-3 and L* >= HIT_MIN,
+// so the comparisons agree.  A NaN fails both compares, as before.)  This replaces the Markstein
+// quotients and their range guards: 2 x (3 + 4) instructions per axis -> 2 x 2.
 __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const RayAx& ax, float e, float ls) {
     bool ok = true;
 #pragma unroll
@@ -583,11 +611,9 @@ __device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const Ray
         const float d = a == 0 ? ax.dx : (a == 1 ? ax.dy : ax.dz);
         const float rc = a == 0 ? ax.rx : (a == 1 ? ax.ry : ax.rz);
         const float nlo = (c - s.w) - o, nhi = (c + s.w) - o;
-        // only compared below: the sign of a zero quotient does not matter
-        const float tlo = div_mk_nz(nlo, d, rc), thi = div_mk_nz(nhi, d, rc);
-        const float tn = d > 0.0f ? tlo : thi, tf = d > 0.0f ? thi : tlo;
-        ok &= mk_num(nlo) && mk_num(nhi);
-        ok &= (tn <= e) && (tf > ls);
+        const float qlo = nlo * rc, qhi = nhi * rc;
+        const float qn = d > 0.0f ? qlo : qhi, qf = d > 0.0f ? qhi : qlo;
+        ok &= (fmaf(fabsf(qn), 0x1p-21f, qn) <= e) && (fmaf(-fabsf(qf), 0x1p-21f, qf) > ls);
     }
     return ok;
 }
@@ -615,6 +641,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
     // (the per-sphere skip branch keeps the compiler from overlapping consecutive iterations).
     auto take = [&](const SphDisc& q, uint32_t i) {
         if (__builtin_expect(__ballot(q.thing2 > 0.0f) == 0, 0)) return;  // v false on every lane
+        RC(RC_ROOTS);
         float l;
         const bool v = sphere_roots<false>(q, &l) & !(l < HIT_MIN);
         any |= v;
@@ -636,6 +663,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
     float root_entry, root_exit;
     const RayAx ax = ray_axes(r);
     if (any && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
+        RC(RC_SLAB);
         // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
         const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
         // (COUNT here means the device-work count: closest_small never runs for the reference's)
@@ -646,6 +674,7 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
             return true;
         }
         const float entry = fmaxf(root_entry, e);
+        RC(RC_FALLBACK);
         bool found;
         const bool fast = sc.fastdiv && origin_fast_ok(r.o);
         if (__builtin_expect(__ballot(!fast) == 0, 1))
@@ -772,6 +801,18 @@ __device__ __forceinline__ uint32_t pass_owner(uint32_t incl, uint32_t total, ui
 // start on neighbouring pixels, so most lanes share their leaf: a pair then reads its primitive
 // from LDS instead of a ref and three gathers from L1 / L2 per (ray, primitive) pair.
 __shared__ float4 g_slab[BLOCK / 64][RT_SLAB_TRIS > 0 ? 3 * RT_SLAB_TRIS : 1];
+// Experiment (RT_SLAB_GLDS = 1, off in the product): the slab filled by
+// LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no ds_write) as three planes of 16-B records
+// — the DMA writes lane i's 16 B at base + 16 i, so one instruction fills 64 consecutive slots of a
+// plane — with the refs beside them; RT_SLAB_TRIS must then be a multiple of 64.
+#ifndef RT_SLAB_GLDS
+#define RT_SLAB_GLDS 0
+#endif
+#if RT_SLAB_GLDS
+static_assert(RT_SLAB_TRIS % 64 == 0, "RT_SLAB_GLDS: RT_SLAB_TRIS must be a multiple of 64");
+__shared__ float4 g_slab_plane[BLOCK / 64][3][RT_SLAB_TRIS];
+__shared__ uint32_t g_slab_ref[BLOCK / 64][RT_SLAB_TRIS];
+#endif
 constexpr uint32_t SLAB_NONE = 0x80000000u;  // a lane's slab delta when its leaf is not staged
 
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
@@ -814,6 +855,20 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 const uint32_t w = fb + lane;
                 const uint32_t fo = list_owner(fincl, w);
                 const uint32_t src = w + __shfl(off - (fincl - lead_n), fo);
+#if RT_SLAB_GLDS
+                // every lane issues (a lane past the staged items loads the first item's record
+                // into its own slot, never read)
+                const uint32_t ref = sc.refs[w < used ? src : __shfl(src, 0)];
+                const float4* pd = prim_data(sc, ref);
+                const uint32_t wv = threadIdx.x >> 6;
+                __builtin_amdgcn_global_load_lds((const void*)(pd + 0),
+                    (__attribute__((address_space(3))) void*)&g_slab_plane[wv][0][fb], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(pd + 1),
+                    (__attribute__((address_space(3))) void*)&g_slab_plane[wv][1][fb], 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(pd + 2),
+                    (__attribute__((address_space(3))) void*)&g_slab_plane[wv][2][fb], 16, 0, 0);
+                if (w < used) g_slab_ref[wv][w] = ref;
+#else
                 if (w < used) {
                     const uint32_t ref = sc.refs[src];
                     const float4* pd = prim_data(sc, ref);
@@ -822,7 +877,11 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                     slab[3 * w + 1] = make_float4(a1.x, a1.y, a1.z, __uint_as_float(ref));
                     slab[3 * w + 2] = a2;
                 }
+#endif
             }
+#if RT_SLAB_GLDS
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has landed in LDS
+#endif
             __builtin_amdgcn_wave_barrier();  // the slab's writes before any lane's reads
         }
         if (staged) sdelta = sbase - (incl - cnt);
@@ -842,11 +901,19 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             uint32_t ref;
             float4 a0, a1, a2;
             if (SLAB && od != SLAB_NONE) {
+#if RT_SLAB_GLDS
+                const uint32_t wv = threadIdx.x >> 6, k = w + od;
+                a0 = g_slab_plane[wv][0][k];
+                a1 = g_slab_plane[wv][1][k];
+                a2 = g_slab_plane[wv][2][k];
+                ref = g_slab_ref[wv][k];
+#else
                 const float4* sp = g_slab[threadIdx.x >> 6] + 3 * (w + od);
                 a0 = sp[0];
                 a1 = sp[1];
                 a2 = sp[2];
                 ref = __float_as_uint(a1.w);
+#endif
             } else {
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
@@ -882,10 +949,19 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
+// Experiment (RT_SCALAR_LEAF_MIN = K > 0, off in the product): in each
+// cooperative round, when at least K lanes hold the first holding lane's leaf (one readfirstlane
+// and one ballot), that leaf is tested on the scalar path — its refs and triangles wave-uniform,
+// loaded by s_load, beside the saturated vector-memory pipeline — against each holder's ray, one
+// ref at a time in leaf order (the first strict minimum of closest_hit.rs:25, as a key), and the
+// holders leave the round's cooperative passes with that key.
+#ifndef RT_SCALAR_LEAF_MIN
+#define RT_SCALAR_LEAF_MIN 0
+#endif
 template <bool FAST, bool RESTART, bool SLAB>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
-                                                  uint32_t* st) {
+                                                  uint32_t* st, const PkScene* ps = nullptr) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0, restart = 0;
     int sp = 0;
@@ -906,13 +982,13 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         } else {
             --sp;
             VC(1, sp ? 2 : 1);
-            const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
+            const uint2 pn = fetch_node_coop(sc, st[sp * BLOCK]);
             float d;
             (void)split_t<FAST>(pn, ax, r, &d);
             node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
             entry = top_t;
             if (sp) {
-                top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
+                top_t = split_t<FAST>(fetch_node_coop(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
                 exit_t = top_t;
             } else {
                 exit_t = root_exit;
@@ -925,7 +1001,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         unsigned long long key0 = ~0ull;
         VC(12, 1);
         if (!done) {
-            uint2 nd = fetch_node(sc, node);
+            uint2 nd = fetch_node_coop(sc, node);
             VC(0, 1);
             pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
@@ -936,9 +1012,17 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 const uint32_t cpair = nd.y >> 2;
                 uint4 pair = make_uint4(0u, 0u, 0u, 0u);
                 if (RT_PAIR_FETCH) {
-                    const uint2* pp = sc.nodes + cpair;
-                    const uint2 c0 = pp[0], c1 = pp[1];
-                    pair = make_uint4(c0.x, c0.y, c1.x, c1.y);
+#if RT_LDS_TOP
+                    if (cpair + 1 < (uint32_t)RT_LDS_TOP) {
+                        const uint2 c0 = g_top[cpair], c1 = g_top[cpair + 1];
+                        pair = make_uint4(c0.x, c0.y, c1.x, c1.y);
+                    } else
+#endif
+                    {
+                        const uint2* pp = sc.nodes + cpair;
+                        const uint2 c0 = pp[0], c1 = pp[1];
+                        pair = make_uint4(c0.x, c0.y, c1.x, c1.y);
+                    }
                 }
                 float d;
                 const float t = split_t<FAST>(nd, ax, r, &d);
@@ -960,7 +1044,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 if (RT_PAIR_FETCH) {
                     nd = node == cpair ? make_uint2(pair.x, pair.y) : make_uint2(pair.z, pair.w);
                 } else {
-                    nd = fetch_node(sc, node);
+                    nd = fetch_node_coop(sc, node);
                 }
             }
             off = nd.y >> 2;
@@ -986,6 +1070,37 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 cnt -= lead;
             }
         }
+#if RT_SCALAR_LEAF_MIN > 0
+        if (ps) {
+            const uint64_t hv = __ballot(cnt > 0);
+            if (hv) {
+                const uint32_t f = (uint32_t)__ffsll((unsigned long long)hv) - 1u;
+                const uint32_t so = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)f);
+                const uint32_t sn = (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)f);
+                const bool mine = cnt > 0 && off == so;  // equal offsets: the same ref list
+                if (__popcll(__ballot(mine)) >= RT_SCALAR_LEAF_MIN) {
+                    unsigned long long k = key0;
+                    for (uint32_t j = 0; j < sn; ++j) {
+                        const uint32_t ref = ps->refs[so + j];
+                        const float4* pd = ps->prim4 + 3 * (size_t)(ref & REF_INDEX_MASK);
+                        const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
+                        if (mine) {
+                            float l = 0.f, bu, bv;
+                            bool h;
+                            if ((ref >> REF_KIND_SHIFT) == K_SPHERE) h = sphere_hit(a0, r, &l);
+                            else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
+                            if (h && l >= HIT_MIN)  // valid and not NaN
+                                k = min(k, ((unsigned long long)__float_as_uint(l) << 32) | (so + j));
+                        }
+                    }
+                    if (mine) {
+                        key0 = k;
+                        cnt = 0;
+                    }
+                }
+            }
+        }
+#endif
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
@@ -1204,9 +1319,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     TM_ADD(8, __popcll(__ballot(in_coop)));
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
-            found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st, ps) || found;
         else
-            found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st, ps) || found;
     }
     TM_ADD(1, TM_NOW() - tm1);
     if (found) return true;
@@ -1496,7 +1611,9 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     }
     if (!hit) return true;  // miss: radiance 0
     if (COUNT) c.hits++;
+    if (!GEN) RC(RC_SHADE_HIT);
     if (h.ref == REF_CUBE) {  // emissive only, no continue (distant_cube_map.rs:22,52-58)
+        if (!GEN) RC(RC_CUBE);
         // (the reference still draws the RR uniform here; the stream ends with the path)
         p.L = p.L + cmul(p.T, cube_emissive(sc, p.ray.d));
         return true;
@@ -1519,11 +1636,15 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     }
     const uint32_t divert = m->divert;
     bool seed_diff = false;
-    if (divert == RT_DIVERT_DIFFSPEC) seed_diff = draw(&p.rng) < m->diffp;  // generate_seed
+    if (divert == RT_DIVERT_DIFFSPEC) {
+        if (!GEN) RC(RC_SEED);
+        seed_diff = draw(&p.rng) < m->diffp;  // generate_seed
+    }
     p.L = p.L + cmul(p.T, ld3(m->em));  // triangles carry em = 0 (generic.rs:86)
     if (sc.debug_single_ray) return true;
     bool atten = false;  // russian_roulette_filter (radiance.rs:74-86)
     if (p.depth > sc.assured_depth) {
+        if (!GEN) RC(RC_RR);
         if (!(draw(&p.rng) < RR_THRES)) return true;
         atten = true;
     }
@@ -1533,12 +1654,16 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     const V3 refl = p.ray.d - (n * 2.0f) * dn;  // spec (interaction.rs:6-9)
     V3 nd;
     if (divert == RT_DIVERT_SPEC || (divert == RT_DIVERT_DIFFSPEC && !seed_diff)) {
+        if (!GEN) RC(RC_SPEC);
         nd = refl;
     } else if (divert == RT_DIVERT_DIELECTRIC) {
+        if (!GEN) RC(RC_DIELECTRIC);
         nd = refract_vec(p.ray.d, n, dn, refl, m->over_in, m->over_out, m->r0, &prob, &p.rng);
     } else {
+        if (!GEN) RC(RC_DIFF);
         nd = diff_vec(p.ray.d, n, dn, &p.rng);
     }
+    if (!GEN && atten && prob != 1.0f) RC(RC_ATTEN_DIV);
     V3 rgb = ld3(m->rgb) * prob;
     // rgb * 1 is rgb, so with p = 1 the attenuated colour is the host's rgb / 0.4
     if (atten) rgb = prob == 1.0f ? ld3(m->rgb_atten) : div3(rgb, RR_THRES);
@@ -1824,6 +1949,12 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         fill_lds_spheres(sc);
         __syncthreads();
     }
+#if RT_LDS_TOP
+    if (GEN) {
+        for (uint32_t i = threadIdx.x; i < (uint32_t)RT_LDS_TOP && i < sc.n_nodes; i += BLOCK) g_top[i] = sc.nodes[i];
+        __syncthreads();
+    }
+#endif
     uint32_t* st = GEN ? dyn_lds + threadIdx.x
                        : a.gstack + (size_t)blockIdx.x * BLOCK * sc.stack_depth + threadIdx.x;
     Ctr<false> c;
@@ -1848,6 +1979,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         constexpr int regen_min = GEN ? RT_REGEN_MIN_GEN : (RT_START_BATCH ? RT_REGEN_MIN_BATCH : RT_REGEN_MIN);
         const bool regen = need && (regen_min <= 1 || __popcll(need) >= regen_min || __ballot(have) == 0);
         if (!GEN && RT_START_BATCH && regen && batch_ok) {
+            RC(RC_REGEN);
             // the n idle lanes take entries st_pos .. st_pos + n - 1 of the batch, making the
             // next batch (the wave's next 64 items) when it runs out
             const uint32_t n = (uint32_t)__popcll(need);
@@ -1862,6 +1994,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             };
             if (idle && r < st_n) take(st_pos + r);  // before the next batch overwrites them
             if (n > st_n) {
+                RC(RC_BATCH);
                 // One counter (a.queue[0] over all the items, whatever a.n_shards): the sphere-only
                 // kernel's grabs are 256+ items (RT_QMIN_SPH), and the shard walk of qgrab cost
                 // walled 1.7% here.
@@ -1966,12 +2099,17 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
             DIAG_WAVE_EXIT(GEN);
             break;
         }
+        if (!GEN) {
+            RC(RC_ITER);
+            if (have) RC_LANES(RC_ITER_LANES);
+        }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
         const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             if (GEN) VC(13, 1);
+            if (!GEN) RC(RC_STORE);
             float* r = a.radiance + 3 * (size_t)slot;
             r[0] = p.L.x;
             r[1] = p.L.y;

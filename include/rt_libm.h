@@ -13,7 +13,8 @@
  * the device computes glibc's float results bit for bit instead of ocml's (which differ by an
  * ulp on some inputs).  Only the ranges the renderer reaches are restated:
  *   - sinf/cosf for |x| < 120 (the renderer's angles are 2*pi*v, v in [0, 1));
- *   - powf(x, 5) for every finite x (the Schlick terms; x in [-eps, 1 + eps]).
+ *   - powf(x, 5) for every finite x (the Schlick terms; x in [-eps, 1 + eps]), with a fast path
+ *     (x^5 in double, exact where it cannot differ from glibc's rounding: rt_powf5_fast).
  * Outside its range rt_sincosf reports failure (the renderer's angles never leave it).
  * The tables are the values of glibc's __sincosf_table, __powf_log2_data and __exp2f_data.
  *
@@ -150,7 +151,7 @@ RT_LIBM_TABLE uint64_t rt_exp2f_tab[32] = {
 #define RT_EXP2F_C2 0x1.62e42ff0c52d6p-1
 
 /* powf(x, 5.0f), as glibc computes it for y = 5 (an odd integer).  Every finite x. */
-RT_LIBM_FN float rt_powf5(float x) {
+RT_LIBM_FN float rt_powf5_glibc(float x) {
     uint32_t ix = rt_libm_asuint(x);
     uint64_t sign_bias = 0;
     if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
@@ -207,6 +208,33 @@ RT_LIBM_FN float rt_powf5(float x) {
     yy = fma(zz, rr2, yy);
     yy = yy * s;
     return (float)yy;
+}
+
+/* The fast path (round 4).  For x in [2^-25, 2], x^5 in double — x * x exact (48 bits), then two
+ * rounded products, within 2^-52 of x^5 — rounds to the correctly rounded float x^5 for every
+ * such x (exhaustive, tools/check_libm.c pow_all).  glibc's powf rounds its own double value yy,
+ * which lies within 2^-32.83 (relative) of x^5 over that range (exhaustive), so it
+ * returns the same float unless x^5 is that close to a midpoint between two floats.  The 29
+ * double-fraction bits the float drops say how far x5 lies from the midpoint: when they are more
+ * than 2^21 + 4 double ulps away from it (2^21 covers 2^-32 of a value in [2^e, 2^(e + 1))), both
+ * x^5 and yy are on x5's side, and the float of x5 is glibc's result.  Otherwise (0.8% of the
+ * floats in the range) and outside the range the caller takes glibc's algorithm.  Returns 0 then. */
+#define RT_POW5_GUARD ((1 << 21) + 4)
+#ifndef RT_LIBM_POW5_FAST
+#define RT_LIBM_POW5_FAST 1  /* 0: glibc's algorithm for every x (A/B builds only) */
+#endif
+RT_LIBM_FN int rt_powf5_fast(float x, float* out) {
+    const double x2 = (double)x * (double)x, x4 = x2 * x2, x5 = x4 * (double)x;
+    const int32_t low = (int32_t)(rt_libm_asuint64(x5) & 0x1fffffffu) - 0x10000000;
+    *out = (float)x5;
+    return (x >= 0x1p-25f && x <= 2.0f) && (low > RT_POW5_GUARD || low < -RT_POW5_GUARD);
+}
+
+/* glibc's powf(x, 5.0f), bit for bit, for every float x (tools/check_libm.c pow_all). */
+RT_LIBM_FN float rt_powf5(float x) {
+    float f;
+    if (RT_LIBM_POW5_FAST && __builtin_expect(rt_powf5_fast(x, &f), 1)) return f;
+    return rt_powf5_glibc(x);
 }
 
 #endif /* RT_LIBM_H */

@@ -107,3 +107,29 @@ def test_shipped_library_has_no_device_printf():
     diag = os.path.join(os.path.dirname(abi.LIB_PATH), "variants", "librt_diag_timing.so")
     if os.path.exists(diag):
         assert b"hostcall" in _gfx950_object(diag)
+
+
+def test_in_return_leaf_quotient_bracket():
+    """trace.hip in_return_leaf (round 4) compares the face distances through q = RN(n * RN(1 / d))
+    and the bounds fma(|q|, 2^-21, q) (upper) / fma(-|q|, 2^-21, q) (lower) instead of the exact
+    quotient RN(n / d) the traversal computes: the exact quotient must lie inside the bracket for
+    every n and every clamped direction d (|d| in [EPS, 1]).  Checked on 2^24 random pairs spread
+    over the exponents the scenes reach (|n| in [2^-40, 2^60]) plus powers of two and ties."""
+    import numpy as np
+
+    rng = np.random.default_rng(7)
+    N = 1 << 24
+    n = (rng.uniform(1, 2, N) * 2.0 ** rng.integers(-40, 60, N)).astype(np.float32)
+    n *= np.where(rng.integers(0, 2, N) == 1, 1, -1).astype(np.float32)
+    d = (rng.uniform(1, 2, N) * 2.0 ** rng.integers(-14, 0, N)).astype(np.float32)  # [2^-14, 1) >= EPS
+    d = np.clip(d, np.float32(1e-4), np.float32(1.0)) * np.where(rng.integers(0, 2, N) == 1, 1, -1).astype(np.float32)
+    n[:64] = np.float32(2.0) ** np.arange(-32, 32, dtype=np.float32)
+    d[:64] = np.float32(1e-4)
+    rc = (np.float32(1.0) / d).astype(np.float32)
+    q = (n * rc).astype(np.float32)
+    t = (n / d).astype(np.float32)  # the traversal's quotient (correctly rounded)
+    # fmaf(|q|, 2^-21, +-q): exact in double (24 + 21 bits), then one rounding to float
+    aq = np.abs(q).astype(np.float64) * 2.0 ** -21
+    up = (q.astype(np.float64) + aq).astype(np.float32)
+    lo = (q.astype(np.float64) - aq).astype(np.float32)
+    assert np.all(t <= up) and np.all(t >= lo)

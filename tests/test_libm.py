@@ -47,5 +47,9 @@ def test_libm_restatement_exhaustive_cpu():
 def test_powf5_every_float_cpu():
     """powf(x, 5) on all 2^32 float bit patterns (negative, subnormal, zero, inf, NaN and the
     overflow / underflow range included), bit for bit against glibc (about 10 s on 8 cores)."""
-    r = _run("check_libm", "pow_all", timeout=600)
+    r = _run("check_libm", "pow_all", timeout=900)
     assert r["powf5_every_float"] == [1 << 32, 0, "0x00000000"], r
+    # the glibc algorithm alone is exact too, and the fast path (x^5 in double, round 4) serves
+    # over 99% of its range [2^-25, 2]
+    assert r["glibc_path_mismatches"] == 0, r
+    assert r["fast_path_taken"] > 0.99 * r["fast_path_range"], r

@@ -51,17 +51,26 @@ static uint32_t hash(uint32_t x) {
 
 int main(int argc, char** argv) {
     if (argc > 1 && strcmp(argv[1], "pow_all") == 0) {
-        unsigned long long bad = 0; uint32_t first = 0;
-#pragma omp parallel for reduction(+ : bad) schedule(dynamic, 1 << 20)
+        /* rt_powf5 (fast path + glibc's algorithm) and each part alone against glibc's powf */
+        unsigned long long bad = 0, fast = 0, fast_range = 0, glibc_bad = 0; uint32_t first = 0;
+#pragma omp parallel for reduction(+ : bad, fast, fast_range, glibc_bad) schedule(dynamic, 1 << 20)
         for (int64_t u = 0; u < (int64_t)1 << 32; ++u) {
             unsigned long long b = 0; uint32_t f = 0;
-            check_pow(flt((uint32_t)u), &b, &f);
+            const float x = flt((uint32_t)u);
+            check_pow(x, &b, &f);
+            float ff;
+            if (x >= 0x1p-25f && x <= 2.0f) ++fast_range;
+            if (rt_powf5_fast(x, &ff)) ++fast;
+            volatile float xv = x, y = 5.0f;
+            if (!same(rt_powf5_glibc(x), powf(xv, y))) ++glibc_bad;
             if (b) { bad += b;
 #pragma omp critical
                 if (!first) first = f; }
         }
-        printf("{\"powf5_every_float\": [%llu, %llu, \"0x%08x\"]}\n", 1ull << 32, bad, first);
-        return bad ? 1 : 0;
+        printf("{\"powf5_every_float\": [%llu, %llu, \"0x%08x\"], \"glibc_path_mismatches\": %llu, "
+               "\"fast_path_taken\": %llu, \"fast_path_range\": %llu}\n",
+               1ull << 32, bad, first, glibc_bad, fast, fast_range);
+        return (bad || glibc_bad) ? 1 : 0;
     }
     const int full = argc > 1 && strcmp(argv[1], "full") == 0;
     const float PI = 3.14159265358979323846f;
