@@ -81,6 +81,7 @@ enum {
     RC_ATTEN_DIV,     // attenuated colour by division (p != 1)
     RC_STORE,         // radiance stores (paths ending)
     RC_CUBE,          // cube-map emission
+    RC_POW_SLOW,      // powf(x, 5) through glibc's path (the fast double-product check failed)
     RC_N = 24
 };
 #if RT_REGION_COUNT

@@ -226,22 +226,6 @@ __shared__ float4 g_lds_sph[RT_LDS_SPHERES];
 __shared__ float4 g_lds_csq[RT_LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
 __shared__ DevMat g_lds_mat[RT_LDS_SPHERES];
 __device__ __forceinline__ uint2 fetch_node(const DevScene& sc, uint32_t i) { return sc.nodes[i]; }
-// Experiment (RT_LDS_TOP = N > 0, off in the product): the first N nodes of
-// the blocked layout — the top of the tree (kd_build.cpp relayout_blocked: 128 nodes ~ 6 levels,
-// 1024 ~ 9) — copied into LDS per workgroup, and the cooperative descent and pops read those
-// nodes from LDS instead of through the vector-memory path.
-#ifndef RT_LDS_TOP
-#define RT_LDS_TOP 0
-#endif
-#if RT_LDS_TOP
-__shared__ uint2 g_top[RT_LDS_TOP];
-#endif
-__device__ __forceinline__ uint2 fetch_node_coop(const DevScene& sc, uint32_t i) {
-#if RT_LDS_TOP
-    if (i < (uint32_t)RT_LDS_TOP) return g_top[i];
-#endif
-    return sc.nodes[i];
-}
 // GEN == false (sphere-only kernel): spheres come from LDS.  The general kernel reads them from
 // global memory.
 template <bool GEN>
@@ -801,18 +785,6 @@ __device__ __forceinline__ uint32_t pass_owner(uint32_t incl, uint32_t total, ui
 // start on neighbouring pixels, so most lanes share their leaf: a pair then reads its primitive
 // from LDS instead of a ref and three gathers from L1 / L2 per (ray, primitive) pair.
 __shared__ float4 g_slab[BLOCK / 64][RT_SLAB_TRIS > 0 ? 3 * RT_SLAB_TRIS : 1];
-// Experiment (RT_SLAB_GLDS = 1, off in the product): the slab filled by
-// LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no ds_write) as three planes of 16-B records
-// — the DMA writes lane i's 16 B at base + 16 i, so one instruction fills 64 consecutive slots of a
-// plane — with the refs beside them; RT_SLAB_TRIS must then be a multiple of 64.
-#ifndef RT_SLAB_GLDS
-#define RT_SLAB_GLDS 0
-#endif
-#if RT_SLAB_GLDS
-static_assert(RT_SLAB_TRIS % 64 == 0, "RT_SLAB_GLDS: RT_SLAB_TRIS must be a multiple of 64");
-__shared__ float4 g_slab_plane[BLOCK / 64][3][RT_SLAB_TRIS];
-__shared__ uint32_t g_slab_ref[BLOCK / 64][RT_SLAB_TRIS];
-#endif
 constexpr uint32_t SLAB_NONE = 0x80000000u;  // a lane's slab delta when its leaf is not staged
 
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
@@ -855,20 +827,6 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 const uint32_t w = fb + lane;
                 const uint32_t fo = list_owner(fincl, w);
                 const uint32_t src = w + __shfl(off - (fincl - lead_n), fo);
-#if RT_SLAB_GLDS
-                // every lane issues (a lane past the staged items loads the first item's record
-                // into its own slot, never read)
-                const uint32_t ref = sc.refs[w < used ? src : __shfl(src, 0)];
-                const float4* pd = prim_data(sc, ref);
-                const uint32_t wv = threadIdx.x >> 6;
-                __builtin_amdgcn_global_load_lds((const void*)(pd + 0),
-                    (__attribute__((address_space(3))) void*)&g_slab_plane[wv][0][fb], 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(pd + 1),
-                    (__attribute__((address_space(3))) void*)&g_slab_plane[wv][1][fb], 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(pd + 2),
-                    (__attribute__((address_space(3))) void*)&g_slab_plane[wv][2][fb], 16, 0, 0);
-                if (w < used) g_slab_ref[wv][w] = ref;
-#else
                 if (w < used) {
                     const uint32_t ref = sc.refs[src];
                     const float4* pd = prim_data(sc, ref);
@@ -877,11 +835,7 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                     slab[3 * w + 1] = make_float4(a1.x, a1.y, a1.z, __uint_as_float(ref));
                     slab[3 * w + 2] = a2;
                 }
-#endif
             }
-#if RT_SLAB_GLDS
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has landed in LDS
-#endif
             __builtin_amdgcn_wave_barrier();  // the slab's writes before any lane's reads
         }
         if (staged) sdelta = sbase - (incl - cnt);
@@ -901,19 +855,11 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
             uint32_t ref;
             float4 a0, a1, a2;
             if (SLAB && od != SLAB_NONE) {
-#if RT_SLAB_GLDS
-                const uint32_t wv = threadIdx.x >> 6, k = w + od;
-                a0 = g_slab_plane[wv][0][k];
-                a1 = g_slab_plane[wv][1][k];
-                a2 = g_slab_plane[wv][2][k];
-                ref = g_slab_ref[wv][k];
-#else
                 const float4* sp = g_slab[threadIdx.x >> 6] + 3 * (w + od);
                 a0 = sp[0];
                 a1 = sp[1];
                 a2 = sp[2];
                 ref = __float_as_uint(a1.w);
-#endif
             } else {
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
@@ -949,19 +895,10 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
-// Experiment (RT_SCALAR_LEAF_MIN = K > 0, off in the product): in each
-// cooperative round, when at least K lanes hold the first holding lane's leaf (one readfirstlane
-// and one ballot), that leaf is tested on the scalar path — its refs and triangles wave-uniform,
-// loaded by s_load, beside the saturated vector-memory pipeline — against each holder's ray, one
-// ref at a time in leaf order (the first strict minimum of closest_hit.rs:25, as a key), and the
-// holders leave the round's cooperative passes with that key.
-#ifndef RT_SCALAR_LEAF_MIN
-#define RT_SCALAR_LEAF_MIN 0
-#endif
 template <bool FAST, bool RESTART, bool SLAB>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
-                                                  uint32_t* st, const PkScene* ps = nullptr) {
+                                                  uint32_t* st) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0, restart = 0;
     int sp = 0;
@@ -982,13 +919,13 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         } else {
             --sp;
             VC(1, sp ? 2 : 1);
-            const uint2 pn = fetch_node_coop(sc, st[sp * BLOCK]);
+            const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
             float d;
             (void)split_t<FAST>(pn, ax, r, &d);
             node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
             entry = top_t;
             if (sp) {
-                top_t = split_t<FAST>(fetch_node_coop(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
+                top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
                 exit_t = top_t;
             } else {
                 exit_t = root_exit;
@@ -1001,7 +938,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         unsigned long long key0 = ~0ull;
         VC(12, 1);
         if (!done) {
-            uint2 nd = fetch_node_coop(sc, node);
+            uint2 nd = fetch_node(sc, node);
             VC(0, 1);
             pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
@@ -1012,12 +949,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 const uint32_t cpair = nd.y >> 2;
                 uint4 pair = make_uint4(0u, 0u, 0u, 0u);
                 if (RT_PAIR_FETCH) {
-#if RT_LDS_TOP
-                    if (cpair + 1 < (uint32_t)RT_LDS_TOP) {
-                        const uint2 c0 = g_top[cpair], c1 = g_top[cpair + 1];
-                        pair = make_uint4(c0.x, c0.y, c1.x, c1.y);
-                    } else
-#endif
                     {
                         const uint2* pp = sc.nodes + cpair;
                         const uint2 c0 = pp[0], c1 = pp[1];
@@ -1044,7 +975,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 if (RT_PAIR_FETCH) {
                     nd = node == cpair ? make_uint2(pair.x, pair.y) : make_uint2(pair.z, pair.w);
                 } else {
-                    nd = fetch_node_coop(sc, node);
+                    nd = fetch_node(sc, node);
                 }
             }
             off = nd.y >> 2;
@@ -1070,37 +1001,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 cnt -= lead;
             }
         }
-#if RT_SCALAR_LEAF_MIN > 0
-        if (ps) {
-            const uint64_t hv = __ballot(cnt > 0);
-            if (hv) {
-                const uint32_t f = (uint32_t)__ffsll((unsigned long long)hv) - 1u;
-                const uint32_t so = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)f);
-                const uint32_t sn = (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)f);
-                const bool mine = cnt > 0 && off == so;  // equal offsets: the same ref list
-                if (__popcll(__ballot(mine)) >= RT_SCALAR_LEAF_MIN) {
-                    unsigned long long k = key0;
-                    for (uint32_t j = 0; j < sn; ++j) {
-                        const uint32_t ref = ps->refs[so + j];
-                        const float4* pd = ps->prim4 + 3 * (size_t)(ref & REF_INDEX_MASK);
-                        const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
-                        if (mine) {
-                            float l = 0.f, bu, bv;
-                            bool h;
-                            if ((ref >> REF_KIND_SHIFT) == K_SPHERE) h = sphere_hit(a0, r, &l);
-                            else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
-                            if (h && l >= HIT_MIN)  // valid and not NaN
-                                k = min(k, ((unsigned long long)__float_as_uint(l) << 32) | (so + j));
-                        }
-                    }
-                    if (mine) {
-                        key0 = k;
-                        cnt = 0;
-                    }
-                }
-            }
-        }
-#endif
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
         const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
@@ -1319,9 +1219,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     TM_ADD(8, __popcll(__ballot(in_coop)));
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
-            found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st, ps) || found;
+            found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
         else
-            found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st, ps) || found;
+            found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
     }
     TM_ADD(1, TM_NOW() - tm1);
     if (found) return true;
@@ -1362,6 +1262,18 @@ __device__ __forceinline__ V3 diff_vec(V3 d, V3 n, float dn, rt_rng_state* rng) 
 // dn = dot(d, n) (= dot(n, d): products commute) and refl = d - 2n(d.n), the mirror direction
 // of :6-9, come from the caller; the mirror about -n is the same vector bit for bit (each
 // negation is exact).
+// glibc's powf(x, 5) (include/rt_libm.h); the diagnostic region build counts the slow path.
+__device__ __forceinline__ float pow5(float x) {
+#if RT_REGION_COUNT
+    float f;
+    if (rt_powf5_fast(x, &f)) return f;
+    RC(RC_POW_SLOW);
+    return rt_powf5_glibc(x);
+#else
+    return rt_powf5(x);
+#endif
+}
+
 __device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float dn, V3 refl, float over_in, float over_out,
                                           float r0, float* p, rt_rng_state* rng) {  // :29-59
     float c_ = dn;
@@ -1373,7 +1285,7 @@ __device__ __forceinline__ V3 refract_vec(V3 d, V3 n, float dn, V3 refl, float o
     if (c22 < 0.0f) { *p = 1.0f; return refl; }
     V3 trns = n_over * d + norm_refr * (n_over * c1 - sqrt_nonneg(c22));  // c22 >= 0 here
     float c = 1.0f - (into ? c1 : dot(trns, n));
-    float re = r0 + (1.0f + r0) * rt_powf5(c);  // glibc's powf(c, 5)
+    float re = r0 + (1.0f + r0) * pow5(c);  // glibc's powf(c, 5)
     float u = draw(rng);
     if (u < re) { *p = re; return refl; }
     *p = 1.0f - re;
@@ -1571,7 +1483,7 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
         rough = mr.y * pr.rough;
     }
     const float r0 = 0.04f + (1.0f - 0.04f) * metal;
-    const float reflectance = r0 + (1.0f - r0) * 1.0f * (1.0f - rt_powf5(fabsf(dot(p.ray.d, n))));
+    const float reflectance = r0 + (1.0f - r0) * 1.0f * (1.0f - pow5(fabsf(dot(p.ray.d, n))));
     const bool should_diff = draw(&p.rng) < 1.0f - reflectance;  // DynDiffSpec::should_diff
     const V3 pos = (p.ray.d * h.l + p.ray.o) + n * EPS;
     if (sc.debug_single_ray) return true;
@@ -1949,12 +1861,6 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         fill_lds_spheres(sc);
         __syncthreads();
     }
-#if RT_LDS_TOP
-    if (GEN) {
-        for (uint32_t i = threadIdx.x; i < (uint32_t)RT_LDS_TOP && i < sc.n_nodes; i += BLOCK) g_top[i] = sc.nodes[i];
-        __syncthreads();
-    }
-#endif
     uint32_t* st = GEN ? dyn_lds + threadIdx.x
                        : a.gstack + (size_t)blockIdx.x * BLOCK * sc.stack_depth + threadIdx.x;
     Ctr<false> c;

@@ -34,6 +34,10 @@ __global__ void k_fma_f32_same(float* out, float s) { BODY("v_fma_f32 %0, %0, %1
 __global__ void k_mul_f32_sq(float* out, float s) { BODY("v_mul_f32 %0, %0, %0 ; %1 %2", float, "v") }
 __global__ void k_mul_f32_same(float* out, float s) { BODY("v_mul_f32 %0, %1, %1 ; %2", float, "v") }
 __global__ void k_rcp_f32(float* out, float s) { BODY("v_rcp_f32 %0, %0 ; %1 %2", float, "v") }
+// packed f32 on 64-bit register pairs (the double only carries the two floats' bits)
+__global__ void k_pk_mul_f32(double* out, double s) { BODY("v_pk_mul_f32 %0, %0, %1 ; %2", double, "v") }
+__global__ void k_pk_add_f32(double* out, double s) { BODY("v_pk_add_f32 %0, %0, %1 ; %2", double, "v") }
+__global__ void k_pk_fma_f32(double* out, double s) { BODY("v_pk_fma_f32 %0, %0, %1, %2", double, "v") }
 
 template <class K, class T>
 static void run(const char* name, K k, T* buf, T s, int blocks) {
@@ -69,6 +73,9 @@ int main() {
     run("v_fma_f64", k_fma_f64, (double*)buf, 1.0, blocks);
     run("v_sqrt_f32", k_sqrt_f32, (float*)buf, 1.0f, blocks);
     run("v_rcp_f32", k_rcp_f32, (float*)buf, 1.0f, blocks);
+    run("v_pk_mul_f32", k_pk_mul_f32, (double*)buf, 1.0, blocks);
+    run("v_pk_add_f32", k_pk_add_f32, (double*)buf, 1.0, blocks);
+    run("v_pk_fma_f32", k_pk_fma_f32, (double*)buf, 1.0, blocks);
     (void)hipFree(buf);
     return 0;
 }

@@ -25,7 +25,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gpu-ray_trace-rust_amd")
 RC_NAMES = ["iter", "iter_lanes", "regen", "batch", "roots", "slab", "fallback", "fb_nodes", "fb_leaves",
-            "shade_hit", "seed", "rr", "spec", "dielectric", "diff", "atten_div", "store", "cube"]
+            "shade_hit", "seed", "rr", "spec", "dielectric", "diff", "atten_div", "store", "cube", "pow_slow"]
 
 CHILD = r"""
 import os, sys
@@ -146,6 +146,8 @@ def event_of(stack, L):
             return "cube"
         if has("diff_vec"):
             return "diff"
+        if has("rt_powf5_glibc"):
+            return "pow_slow"
         if has("refract_vec"):
             return "dielectric"
         if has("div3"):
@@ -178,8 +180,8 @@ def event_of(stack, L):
 
 def anchors():
     L = {"ballot": src_line("__ballot(q.thing2 > 0.0f) == 0"),
-         "pair0": src_line("for (; i + 1 < sc.n_spheres; i += 2) {"),
-         "pair1": src_line("for (; i + 1 < sc.n_spheres; i += 2) {") + 5,
+         "pair0": src_line("const SphDisc qa = sphere_disc(sa, sa.w, r)") - 2,
+         "pair1": src_line("const SphDisc qa = sphere_disc(sa, sa.w, r)") + 3,
          "slab0": src_line("RC(RC_SLAB)") - 1, "slab1": src_line("RC(RC_FALLBACK)") + 8,
          "seed": src_line("seed_diff = draw(&p.rng) < m->diffp"),
          "rr0": src_line("russian_roulette_filter"), "rr1": src_line("russian_roulette_filter") + 5,
