@@ -178,8 +178,10 @@ def test_committed_counters_belong_to_this_build():
         d = json.load(open(p))
         if d.get("build_id") == bid:
             found.setdefault(d.get("scene"), set()).add(d.get("samples_per_launch"))
-    # the bench's configs (bench.py CONFIGS and the walled headline) at their launch shapes
-    want = {"walled": 720_000_000, "a380": 720_000, "biplane": 7_200_000, "spaceship_r1": 419_430_400,
+    # the bench's configs (bench.py CONFIGS and the walled headline) at their launch shapes: a
+    # config's batches are traced in groups of up to bench.GROUP_ITEMS samples (a380: 10 batches of
+    # 1 spp in one launch, biplane: 2 batches of 10 spp)
+    want = {"walled": 720_000_000, "a380": 7_200_000, "biplane": 14_400_000, "spaceship_r1": 419_430_400,
             "triangles": 7_200_000}
     missing = {s: n for s, n in want.items() if n not in found.get(s, set())}
     assert not missing, f"no committed counters of build {bid} for {missing}: re-profile"
