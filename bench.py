@@ -76,8 +76,9 @@ BYTES = {"nodes": 8, "leaf_refs": 4, "sphere_tests": 16, "tri_tests": 36, "hits"
 CPU_SPP = {"walled": 20, "biplane": 10, "a380": 2, "spaceship_r1@4096": 1, "spaceship_r1": 2, "triangles": 10}
 # ... over every k-th row only where a full frame takes more than ~10 s of CPU per call
 CPU_ROWS_STEP = {"spaceship_r1@4096": 4}
-# ... and more samples where BASELINE.md §2's count takes well under a second (timer noise)
-CPU_SPP_MIN_RUN = {"triangles": 100}
+# ... and more samples where BASELINE.md §2's count takes well under a second: each call then
+# lasts a few seconds (round 4: triangles at 100 spp, 0.7-2 s per call, spread 2.1 over 3 calls)
+CPU_SPP_MIN_RUN = {"triangles": 600}
 # BASELINE.json configs timed beside the headline at N = 1: name -> (scene, total spp, batch,
 # width, height, timed repetitions of the whole config, warmup repetitions)
 CONFIGS = {

@@ -149,27 +149,25 @@ __device__ __forceinline__ V3 div3(V3 a, float b) {
     if (__builtin_expect(!(mk_range(b) && mk_num(a.x) && mk_num(a.y) && mk_num(a.z)), 0)) q = a / b;
     return q;
 }
-// sqrtf(x), bit for bit: v_sqrt_f32 and the +-1 ulp FMA correction of hipcc's IEEE sequence,
-// without its tiny-input scaling and class check — equal to sqrtf for x in {-0, +0} and every
-// x in [2^-80, +inf] (exhaustive, tools/check_exact_ops.hip; below 2^-80 it is not).
+// sqrtf(x), bit for bit, for every x in [2^-80, FLT_MAX] (exhaustive, tools/check_exact_ops.hip;
+// below 2^-80, at 0 and at +inf it is not): Markstein's correction of s = x * rsq(x) with one
+// rounding, s + (x - s^2) * rsq(x) / 2 — five instructions instead of hipcc's IEEE sequence.
 __device__ __forceinline__ float sqrt_rn(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
-    const float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
-    return fmaf(-su, s, x) > 0.0f ? su : r;
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
+    return fmaf(fmaf(-s, s, x), 0.5f * y, s);
 }
-// sqrtf(x) for x >= -0 (an fmaxf(y, 0), a dot(a, a), a uniform draw).  bits - 1 wraps for +0
-// and is >= 0x7fffffff for -0, so one compare sends exactly (0, 2^-80) to sqrtf — a divergent
-// branch no lane normally takes.  (A NaN x gives a NaN either way.)
+// sqrtf(x) for x >= -0 (an fmaxf(y, 0), a dot(a, a), a uniform draw): one compare sends ±0,
+// (0, 2^-80), +inf and NaN to sqrtf — a divergent branch no lane normally takes.
 __device__ __forceinline__ float sqrt_nonneg(float x) {
     float s = sqrt_rn(x);
-    if (__builtin_expect(__float_as_uint(x) - 1u < (47u << 23) - 1u, 0)) s = sqrtf(x);
+    if (__builtin_expect(__float_as_uint(x) - (47u << 23) >= 0x7f800000u - (47u << 23), 0)) s = sqrtf(x);
     return s;
 }
-// sqrtf of a uniform draw u or of 1 - u: both are 0 or >= 2^-24 (rt_rng.h's (x >> 8) * 2^-24,
-// u <= 1 - 2^-24), inside sqrt_rn's exact range, so no tiny-input guard is needed.
+// sqrtf of a uniform draw u or of 1 - u: 0 or in [2^-24, 1] (rt_rng.h's (x >> 8) * 2^-24,
+// u <= 1 - 2^-24), inside sqrt_rn's exact range but for 0.
 __device__ __forceinline__ float sqrt_draw(float x) {
-    return sqrt_rn(x);
+    return x == 0.0f ? x : sqrt_rn(x);
 }
 // nalgebra normalize: a / |a| per component.  div3's guard, specialised: |a_i| < 2^60 follows
 // from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs to be

@@ -9,14 +9,18 @@
  * Appendix B).  f32 draws keep rand 0.8's `Standard` mapping for f32: (u32 >> 8) * 2^-24,
  * uniform on [0, 1) with 24 significant bits.
  *
- * Generator: pcg32 (O'Neill 2014, "PCG-XSH-RR 64/32"): a 64-bit LCG state
- * (x <- x * 6364136223846793005 + 1442695040888963407 mod 2^64, period 2^64) with the XSH-RR
- * output permutation of the state before the step.  A stream's start state is a bijective
- * 64-bit hash (the SplitMix64 finalizer, Steele et al. 2014) of the seed, the pixel and the
- * sample, so distinct samples of one pixel start at distinct states.  With n streams of L draws
- * at random places on the one 2^64 cycle, a stream shares draws with about 2 n L / 2^64 others:
- * 5.5e-8 for spaceship_r1 at 4096^2 x 1000 spp (n = 1.7e10 streams, L ~ 30), i.e. ~470 pairs in
- * all, against ~240 overlapping streams for EVERY stream with round 1's 32-bit state.
+ * Generator: xoroshiro64* (Blackman & Vigna 2018, "Scrambled linear pseudorandom number
+ * generators"): a 64-bit xorshift-rotate state of two 32-bit words (period 2^64 - 1), output the
+ * first word times 0x9E3779BB.  Its lowest output bits are weak; the f32 draws use the top 24.
+ * It replaced pcg32 (a 64-bit LCG with XSH-RR output) in round 4: one 32-bit multiply per draw
+ * instead of a 64 x 64-bit multiply-add, for the same state size and period.  A
+ * stream's start state is a bijective 64-bit hash (the SplitMix64 finalizer, Steele et al. 2014)
+ * of the seed, the pixel and the sample, so distinct samples of one pixel start at distinct
+ * states (but for the all-zero hash, a fixed point of the generator, which is replaced by a
+ * constant that one other input also hashes to).  With n
+ * streams of L draws at random places on the one 2^64 - 1 cycle, a stream shares draws with
+ * about 2 n L / 2^64 others: 5.5e-8 for spaceship_r1 at 4096^2 x 1000 spp (n = 1.7e10 streams,
+ * L ~ 30), i.e. ~470 pairs in all.
  *
  * Plain C; compiled unchanged by gcc (oracle) and hipcc (gfx950 device code).
  */
@@ -30,9 +34,6 @@
 #else
 #define RT_RNG_FN static inline
 #endif
-
-#define RT_RNG_MUL 6364136223846793005ull
-#define RT_RNG_INC 1442695040888963407ull
 
 typedef uint64_t rt_rng_state;
 
@@ -50,18 +51,22 @@ RT_RNG_FN uint64_t rt_rng_mix64(uint64_t z) {
 RT_RNG_FN uint64_t rt_rng_pixel_key(uint64_t seed, uint32_t pixel) {
     return rt_rng_mix64(seed + 0x9e3779b97f4a7c15ull * ((uint64_t)pixel + 1u));
 }
-RT_RNG_FN rt_rng_state rt_rng_init_key(uint64_t key, uint64_t sample) { return rt_rng_mix64(key ^ sample); }
+RT_RNG_FN rt_rng_state rt_rng_init_key(uint64_t key, uint64_t sample) {
+    const uint64_t z = rt_rng_mix64(key ^ sample);
+    return z ? z : 0x9e3779b97f4a7c15ull;  /* mix64(0) = 0 is xoroshiro's fixed point */
+}
 RT_RNG_FN rt_rng_state rt_rng_init(uint64_t seed, uint32_t pixel, uint64_t sample) {
     return rt_rng_init_key(rt_rng_pixel_key(seed, pixel), sample);
 }
 
-/* Next u32 of the stream (XSH-RR of the current state); advances *state. */
+/* Next u32 of the stream (xoroshiro64*: state = s1 << 32 | s0); advances *state. */
+RT_RNG_FN uint32_t rt_rng_rotl32(uint32_t x, uint32_t k) { return (x << k) | (x >> (32u - k)); }
 RT_RNG_FN uint32_t rt_rng_next_u32(rt_rng_state* state) {
-    const uint64_t x = *state;
-    *state = x * RT_RNG_MUL + RT_RNG_INC;
-    const uint32_t xs = (uint32_t)(((x >> 18u) ^ x) >> 27u);
-    const uint32_t rot = (uint32_t)(x >> 59u);
-    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+    const uint32_t s0 = (uint32_t)*state, s1 = (uint32_t)(*state >> 32) ^ s0;
+    const uint32_t out = s0 * 0x9E3779BBu;
+    const uint32_t n0 = rt_rng_rotl32(s0, 26) ^ s1 ^ (s1 << 9), n1 = rt_rng_rotl32(s1, 13);
+    *state = ((uint64_t)n1 << 32) | n0;
+    return out;
 }
 
 /* rand 0.8 Standard f32: (u32 >> 8) * 2^-24 in [0, 1). */

@@ -1,5 +1,5 @@
 // Exhaustive / large-sample checks, on the GPU, of the fast exact-arithmetic identities the
-// trace kernel relies on (trace.hip: rcp_exact, div_exact, sincos).  Each compares against the
+// trace kernel relies on (trace.hip: rcp_exact, div_exact, sqrt_rn, sincos).  Each compares against the
 // IEEE operation the kernel would otherwise issue (hipcc's correctly rounded 1.0f/b, a/b) or
 // against the separate ocml calls.  Usage: check_exact_ops  (prints one JSON line; exit 1 on any
 // mismatch).  Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o check_exact_ops <this>
@@ -86,10 +86,10 @@ __global__ void k_norm(Stats* s, uint32_t rounds) {
     atomicAdd(&s->tested, n);
 }
 
-// sqrt_rn(x) = v_sqrt_f32 + the +-1 ulp FMA correction (trace.hip), without hipcc's denormal
-// scaling and class check: == sqrtf(x) for every x in [lo, +inf] (bit patterns), lo = 0 for
-// the full check; the per-range counts locate any failure
-__device__ __forceinline__ float sqrt_rn(float x) {
+// sqrt_fix(x) = v_sqrt_f32 + the +-1 ulp FMA correction (the kernels' sqrt_rn until round 4),
+// without hipcc's denormal scaling and class check: == sqrtf(x) for every x in [lo, +inf] (bit
+// patterns), lo = 0 for the full check; the per-range counts locate any failure
+__device__ __forceinline__ float sqrt_fix(float x) {
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
     float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
@@ -106,7 +106,48 @@ __global__ void k_sqrt(Stats* s, uint32_t lo_bits) {
         (void)ex;
         const float x = __uint_as_float(bits);
         ++n;
-        if (__float_as_uint(sqrt_rn(x)) != __float_as_uint(sqrtf(x))) record(s, bits);
+        if (__float_as_uint(sqrt_fix(x)) != __float_as_uint(sqrtf(x))) record(s, bits);
+    }
+    atomicAdd(&s->tested, n);
+}
+
+// sqrt_rn(x) of trace.hip (round 4): the reciprocal square root's Newton correction of
+// s = x * rsq(x) with one rounding, s + (x - s^2) * rsq(x) / 2 (Markstein): 5 instructions
+// instead of sqrt_fix's 9; == sqrtf(x) for every x in [2^-80, FLT_MAX]
+__device__ __forceinline__ float sqrt_rsq(float x) {
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
+    const float r = fmaf(-s, s, x);
+    return fmaf(r, 0.5f * y, s);
+}
+__global__ void k_sqrt_rsq(Stats* s, uint32_t lo_bits, uint32_t hi_bits) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long n = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (1ull << 31); i += stride) {
+        const uint32_t bits = (uint32_t)i;
+        if (bits < lo_bits || bits > hi_bits) continue;
+        const float x = __uint_as_float(bits);
+        ++n;
+        if (__float_as_uint(sqrt_rsq(x)) != __float_as_uint(sqrtf(x))) record(s, bits);
+    }
+    atomicAdd(&s->tested, n);
+}
+
+// normalize's reciprocal from the square root's rsq: n = sqrt_rn(d), y = rsq(d) ~ 1/n, and
+// rcp_from_rsq = fma(fma(-n, y, 1), y, y) == 1.0f / n for every d in [lo, hi] (bit patterns)
+__global__ void k_rcp_rsq(Stats* s, uint32_t lo_bits, uint32_t hi_bits) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long n = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (1ull << 31); i += stride) {
+        const uint32_t bits = (uint32_t)i;
+        if (bits < lo_bits || bits > hi_bits) continue;
+        const float d = __uint_as_float(bits);
+        const float y = __builtin_amdgcn_rsqf(d);
+        const float sq = d * y;
+        const float nn = fmaf(fmaf(-sq, sq, d), 0.5f * y, sq);
+        const float r = fmaf(fmaf(-nn, y, 1.0f), y, y);
+        ++n;
+        if (__float_as_uint(r) != __float_as_uint(1.0f / nn)) record(s, bits);
     }
     atomicAdd(&s->tested, n);
 }
@@ -135,8 +176,8 @@ static int report(const char* name, Stats* d) {
 
 int main() {
     Stats* d;
-    if (hipMalloc(&d, 7 * sizeof(Stats)) != hipSuccess) return 2;
-    (void)hipMemset(d, 0, 7 * sizeof(Stats));
+    if (hipMalloc(&d, 10 * sizeof(Stats)) != hipSuccess) return 2;
+    (void)hipMemset(d, 0, 10 * sizeof(Stats));
     // reciprocal over |b| in [2^-60, 2^60]: biased exponents 67..187
     hipLaunchKernelGGL(k_rcp, dim3(8192), dim3(256), 0, 0, d + 0, 67u, 187u);
     hipLaunchKernelGGL(k_div, dim3(8192), dim3(256), 0, 0, d + 1, 2048u);
@@ -145,6 +186,10 @@ int main() {
     hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, d + 4, 47u << 23);  // [2^-80, inf]
     hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, d + 5, 1u << 23);   // normals
     hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, d + 6, 0u);         // everything >= 0
+    hipLaunchKernelGGL(k_sqrt_rsq, dim3(8192), dim3(256), 0, 0, d + 7, 47u << 23, 0x7f7fffffu);  // [2^-80, max]
+    hipLaunchKernelGGL(k_sqrt_rsq, dim3(8192), dim3(256), 0, 0, d + 8, 1u << 23, 0x7f7fffffu);   // normals
+    // d = a.a of normalize with n = sqrt(d) in normalize's exact range [2^-60, 2^60): d in [2^-120, 2^120)
+    hipLaunchKernelGGL(k_rcp_rsq, dim3(8192), dim3(256), 0, 0, d + 9, 7u << 23, 247u << 23);
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     int bad = 0;
     std::printf("{");
@@ -156,11 +201,17 @@ int main() {
     std::printf(", ");
     bad |= report("sincosf_vs_sinf_cosf", d + 3);
     std::printf(", ");
-    bad |= report("sqrt_rn_2^-80_to_inf", d + 4);
+    bad |= report("sqrt_fix_2^-80_to_inf", d + 4);
     std::printf(", ");
-    (void)report("sqrt_rn_normal_to_inf_info", d + 5);  // informational: fails below 2^-80
+    (void)report("sqrt_fix_normal_to_inf_info", d + 5);  // informational: fails below 2^-80
     std::printf(", ");
-    (void)report("sqrt_rn_all_nonneg_info", d + 6);
+    (void)report("sqrt_fix_all_nonneg_info", d + 6);
+    std::printf(", ");
+    bad |= report("sqrt_rn_rsq_2^-80_to_max", d + 7);
+    std::printf(", ");
+    (void)report("sqrt_rn_rsq_normal_to_max_info", d + 8);  // informational: fails below 2^-80
+    std::printf(", ");
+    (void)report("rcp_from_rsq_candidate_d_2^-120_2^120", d + 9);
     std::printf("}\n");
     (void)hipFree(d);
     return bad;

@@ -26,13 +26,14 @@ for p in ("gpu-ray_trace-rust_amd", "oracle", "tests"):
 # lane-operations per event (trace.hip / rt_rng.h / rt_libm.h; see the comments for each)
 OPS = {
     # per sample: stream start mix64(key ^ sample) = 64-bit xor (2), three shift-xor rounds (4
-    # each), two 64x64 multiplies by constants (6 each); pixel x, y from the table word (2);
+    # each), two 64x64 multiplies by constants (6 each), the zero-state guard (2); pixel x, y
+    # from the table word (2);
     # camera_base_dir: 2 x (cvt, sub, mul) + 6 mul + 6 add; jitter: 2 sub, 12 mul, 6 add; the
     # fold: 3 x (mul, add, div), n + 1, cvt n
-    "sample": 26 + 2 + 18 + 20 + 11,
-    # per draw (rt_rng_next_f32): 64-bit LCG step (6 for the multiply, 2 for the add), XSH-RR
-    # (64-bit shift 2, xor 2, shift 1, rotate amount 1, rotate 1), >> 8, cvt, * 2^-24
-    "draw": 8 + 7 + 3,
+    "sample": 26 + 2 + 2 + 18 + 20 + 11,
+    # per draw (rt_rng_next_f32): xoroshiro64* (round 4): the output multiply, s1 ^ s0, two
+    # rotates, s1 << 9, two xors; >> 8, cvt, * 2^-24
+    "draw": 7 + 3,
     # per segment: normalize the direction (dot 5, sqrt, 3 div)
     "segment": 9,
     # per sphere and segment: sphere_disc, o - c (3), two dots (10), - r^2, dir^2 - consts (2),

@@ -45,7 +45,7 @@ def main():
             else:
                 os.environ[k] = v
     res = {n: [] for n in a.names}
-    ref = None
+    ref = prev = None
     for r in range(a.rounds + 1):
         for n, (ctx, loaded) in ctxs.items():
             w, h = int(loaded.info.width), int(loaded.info.height)
@@ -56,7 +56,9 @@ def main():
                 if ref is None:
                     ref = img
                 same = bool((img == ref).all())
-                print(f"{n}: identical to {a.names[0]}: {same}", flush=True)
+                same_prev = bool((img == prev).all()) if prev is not None else True
+                prev = img
+                print(f"{n}: identical to {a.names[0]}: {same} (to the previous variant: {same_prev})", flush=True)
                 continue
             res[n].append(w * h * a.spp / (ctx.last_kernel_ms() * 1e-3) / 1e6)
     for n, v in res.items():

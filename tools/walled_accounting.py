@@ -212,24 +212,36 @@ def table(path, sq_valu):
                roots_pair=n["roots"] * pairs / n_spheres, roots_rem=n["roots"] * (n_spheres - 2 * pairs) / n_spheres)
     per_region, per_event, unvoted = {}, {}, 0
     total = 0.0
+    prev_ev, prev_falls = None, False
     for pc0, ins in bl:
         votes = {}
         for pc, mn, st, ops in ins:
-            if mn.startswith("v_"):
+            # compiler-made instructions (line 0 in the innermost frame: copies, spills, merged
+            # tails) do not vote; they run where their block runs
+            if mn.startswith("v_") and st and st[0][1] != 0:
                 e = event_of(st, L)
                 if e:
                     votes[e] = votes.get(e, 0) + 1
         valu = [(pc, mn, st) for pc, mn, st, ops in ins if mn.startswith("v_")]
+        falls = not ins[-1][1].startswith(("s_branch", "s_endpgm", "s_setpc"))
+        if votes:
+            ev = max(votes, key=votes.get)
+        elif prev_falls and prev_ev:
+            ev = prev_ev  # a block of compiler-made instructions: its fall-through predecessor's event
+        else:
+            ev = None
+        prev_ev, prev_falls = ev, falls
         if not valu:
             continue
-        if not votes:
+        if ev is None and not any(mn.startswith("v_sqrt_f32") for _, mn, _ in valu):
             unvoted += len(valu)
             continue
-        ev = max(votes, key=votes.get)
+        if ev is None:
+            ev = "cold"  # hipcc's sqrtf behind sqrt_nonneg's guard: its compiler-made copies
         # out-of-line exactness fallbacks (IEEE division, sqrtf's tiny-input scaling): the guarded
         # branches no lane normally takes; counted as not executed
         if any(mn.startswith(("v_div_scale", "v_div_fmas", "v_div_fixup")) for _, mn, _, _ in ins) or \
-                (any(mn.startswith("v_cmp_class") for _, mn, _, _ in ins) and
+                (any(mn.startswith(("v_cmp_class", "v_sqrt_f32")) for _, mn, _, _ in ins) and
                  any("0x4f800000" in ops for _, _, _, ops in ins)):
             ev = "cold"
         c = cnt.get(ev, 0)
