@@ -141,3 +141,53 @@ def test_rng_stream_contract(oracle):
     other = np.zeros(4096, np.float32)
     oracle.lib().oracle_rng_stream(0x5EED0001, 8, 3, 4096, _fp(other))
     assert not np.array_equal(out, other)
+
+
+def _mix64(z):
+    m = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def test_rng_is_xoroshiro64star(oracle):
+    """rt_rng.h's draws are the published xoroshiro64* (Blackman & Vigna 2018: out = s0 * 0x9E3779BB;
+    s1 ^= s0; s0 = rotl(s0, 26) ^ s1 ^ (s1 << 9); s1 = rotl(s1, 13)) started at the SplitMix64 hash of
+    (seed, pixel, sample), mapped to f32 as rand 0.8's Standard: (u32 >> 8) * 2^-24 — restated here
+    in plain Python integers."""
+    m32, m64 = (1 << 32) - 1, (1 << 64) - 1
+    rotl = lambda x, k: ((x << k) | (x >> (32 - k))) & m32  # noqa: E731
+    for seed, pixel, sample in ((0x5EED0001, 7, 3), (0, 0, 0), (2**64 - 1, 719_999, 2**40 + 5)):
+        key = _mix64((seed + 0x9E3779B97F4A7C15 * (pixel + 1)) & m64)
+        st = _mix64(key ^ sample) or 0x9E3779B97F4A7C15
+        s0, s1 = st & m32, st >> 32
+        want = []
+        for _ in range(64):
+            out = (s0 * 0x9E3779BB) & m32
+            want.append(np.float32((out >> 8) * 2.0**-24))
+            s1 ^= s0
+            s0 = rotl(s0, 26) ^ s1 ^ ((s1 << 9) & m32)
+            s1 = rotl(s1, 13)
+        got = np.zeros(64, np.float32)
+        oracle.lib().oracle_rng_stream(C.c_uint64(seed), pixel, C.c_uint64(sample), 64, _fp(got))
+        assert np.array_equal(got, np.array(want, np.float32)), (seed, pixel, sample)
+
+
+def test_rng_stream_statistics(oracle):
+    """Uniformity and serial independence of the f32 draws over many (pixel, sample) streams: the
+    mean and variance of U[0, 1), lag-1 correlation within a stream and correlation between the
+    first draws of neighbouring samples, each within 5 sigma of its expectation."""
+    n_streams, L = 4096, 32
+    draws = np.zeros((n_streams, L), np.float32)
+    for k in range(n_streams):
+        oracle.lib().oracle_rng_stream(C.c_uint64(0x5EED0001), k % 64, C.c_uint64(k // 64), L,
+                                       _fp(draws[k]))
+    x = draws.astype(np.float64)
+    n = x.size
+    assert abs(x.mean() - 0.5) < 5 * np.sqrt(1 / 12 / n)
+    assert abs(x.var() - 1 / 12) < 5 * np.sqrt(1 / 180 / n)
+    lag = np.corrcoef(x[:, :-1].ravel(), x[:, 1:].ravel())[0, 1]
+    assert abs(lag) < 5 / np.sqrt(n)
+    first = x[:, 0].reshape(64, 64)  # [sample][pixel]
+    across = np.corrcoef(first[:-1].ravel(), first[1:].ravel())[0, 1]
+    assert abs(across) < 5 / np.sqrt(first.size)
