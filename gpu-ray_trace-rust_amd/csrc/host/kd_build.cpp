@@ -174,12 +174,20 @@ struct Frontier {
 // a level's concatenated element lists are indexed by uint32.  `budget` counts the nodes and refs
 // of the whole build (all threads): past 2^30 of either the build stops with RT_ERR_OOM instead of
 // growing to the end (a tree whose elements straddle every split copies them at every level).
+// RT_DEBUG_KD_BUDGET lowers the limit (tests/test_kd.py reaches it on a small scene).
 struct BuildBudget {
     std::atomic<uint64_t> nodes{0}, refs{0};
     std::atomic<bool> over{false};
+    uint64_t limit = 1ull << 30;
+    BuildBudget() {
+        if (const char* e = std::getenv("RT_DEBUG_KD_BUDGET")) {
+            const unsigned long long v = std::strtoull(e, nullptr, 10);
+            if (v > 0 && v < limit) limit = v;
+        }
+    }
     bool charge(uint64_t n, uint64_t r) {
         if (over.load(std::memory_order_relaxed)) return false;
-        if (nodes.fetch_add(n) + n >= (1ull << 30) || refs.fetch_add(r) + r >= (1ull << 30)) over = true;
+        if (nodes.fetch_add(n) + n >= limit || refs.fetch_add(r) + r >= limit) over = true;
         return !over.load(std::memory_order_relaxed);
     }
 };
