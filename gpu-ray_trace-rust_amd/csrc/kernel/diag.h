@@ -82,6 +82,8 @@ enum {
     RC_STORE,         // radiance stores (paths ending)
     RC_CUBE,          // cube-map emission
     RC_POW_SLOW,      // powf(x, 5) through glibc's path (the fast double-product check failed)
+    RC_ROOTS_USEFUL,  // closest_small: roots executions where some lane's length becomes the running best
+    RC_ROOTS_FRONT,   // ... where some lane meets the sphere ahead of its origin (not both roots behind it)
     RC_N = 24
 };
 #if RT_REGION_COUNT

@@ -628,6 +628,10 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
         const bool v = sphere_roots<false>(q, &l) & !(l < HIT_MIN);
         any |= v;
         const bool better = v & (l < ls);  // first minimum in renderable order (closest_hit.rs:25)
+#if RT_REGION_COUNT
+        if (__ballot(better)) RC(RC_ROOTS_USEFUL);
+        if (__ballot(q.thing2 > 0.0f && !(q.dir > 0.0f && q.dir * q.dir > q.thing2))) RC(RC_ROOTS_FRONT);
+#endif
         imin = better ? i : imin;
         ls = better ? l : ls;
     };

@@ -25,7 +25,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gpu-ray_trace-rust_amd")
 RC_NAMES = ["iter", "iter_lanes", "regen", "batch", "roots", "slab", "fallback", "fb_nodes", "fb_leaves",
-            "shade_hit", "seed", "rr", "spec", "dielectric", "diff", "atten_div", "store", "cube", "pow_slow"]
+            "shade_hit", "seed", "rr", "spec", "dielectric", "diff", "atten_div", "store", "cube", "pow_slow", "roots_useful", "roots_front"]
 
 CHILD = r"""
 import os, sys
