@@ -4,9 +4,12 @@ branch that made the work unreachable) renders nothing and returns success; the 
 catch that only for the scenes that reach it, so this checks every instantiation at build time.
 Format: the .hip_fatbin section is a clang offload bundle ("__CLANG_OFFLOAD_BUNDLE__", entry
 count, then offset / size / target triple per entry) holding an AMDGPU ELF per target."""
+import os
 import struct
 
 import pytest
+
+from conftest import PKG
 
 
 def _sections(b):
@@ -133,3 +136,25 @@ def test_in_return_leaf_quotient_bracket():
     up = (q.astype(np.float64) + aq).astype(np.float32)
     lo = (q.astype(np.float64) - aq).astype(np.float32)
     assert np.all(t <= up) and np.all(t >= lo)
+
+
+@pytest.mark.gpu
+def test_exact_arithmetic_identities_on_gfx950(gpu_available):
+    """lib/check_exact_ops (tools/check_exact_ops.hip) on the GPU: rcp_exact over every normal
+    |b| in [2^-60, 2^60], the Markstein quotient on 4.3e9 random pairs and 2.1e9 normalize-shaped
+    ones, sincosf == (sinf, cosf) on every angle a draw forms, and both square roots — the
+    v_sqrt_f32 fix-up and the kernel's sqrt_rn (x * rsq(x) with one FMA correction) — on every
+    float in [2^-80, FLT_MAX]: 0 mismatches against the IEEE operations."""
+    import json
+    import subprocess
+
+    exe = os.path.join(PKG, "lib", "check_exact_ops")
+    if not os.path.exists(exe):
+        pytest.fail("lib/check_exact_ops not built (make -C gpu-ray_trace-rust_amd)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("rcp_exact_all_normal_2^-60_2^60", "markstein_div_random_pairs", "normalize_quotients",
+              "sincosf_vs_sinf_cosf", "sqrt_fix_2^-80_to_inf", "sqrt_rn_rsq_2^-80_to_max"):
+        assert d[k]["tested"] > 0 and d[k]["bad"] == 0, (k, d[k])
+    assert d["sqrt_rn_rsq_2^-80_to_max"]["tested"] == (0x7F7FFFFF - (47 << 23) + 1), d
+    assert r.returncode == 0, r.stdout[-500:]
