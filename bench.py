@@ -78,7 +78,7 @@ CPU_SPP = {"walled": 20, "biplane": 10, "a380": 2, "spaceship_r1@4096": 1, "spac
 CPU_ROWS_STEP = {"spaceship_r1@4096": 4}
 # ... and more samples where BASELINE.md §2's count takes well under a second: each call then
 # lasts a few seconds (round 4: triangles at 100 spp, 0.7-2 s per call, spread 2.1 over 3 calls)
-CPU_SPP_MIN_RUN = {"triangles": 600}
+CPU_SPP_MIN_RUN = {"triangles": 600, "a380": 8}  # a380 at 2 spp: 0.65 s per call
 # BASELINE.json configs timed beside the headline at N = 1: name -> (scene, total spp, batch,
 # width, height, timed repetitions of the whole config, warmup repetitions)
 CONFIGS = {
