@@ -203,6 +203,8 @@ static int build_subtree(const std::vector<Renderable>& rs, const std::vector<fl
     for (uint32_t depth = depth0; !items.empty(); ++depth) {
         nxt.clear();
         nitems.clear();
+        // the level's nodes and refs are charged to the shared budget once, at its end
+        uint64_t lvl_nodes = 0, lvl_refs = 0;
         const uint32_t axis = depth % 3;
         for (const Item& it : items) {
             SubNode& nd = out->nodes[it.node];
@@ -216,7 +218,7 @@ static int build_subtree(const std::vector<Renderable>& rs, const std::vector<fl
                 nd.a = n;
                 nd.axis = RT_KD_LEAF;
                 nd.ref_off = (uint32_t)out->refs.size();
-                if (!budget->charge(0, n)) return RT_ERR_OOM;
+                lvl_refs += n;
                 out->refs.insert(out->refs.end(), cur.begin() + it.begin, cur.begin() + it.end);
                 if (depth > out->max_leaf_depth) out->max_leaf_depth = depth;
                 continue;
@@ -234,12 +236,14 @@ static int build_subtree(const std::vector<Renderable>& rs, const std::vector<fl
             const uint32_t hb = (uint32_t)nxt.size();
             for (uint32_t k = it.begin; k < it.end; ++k)
                 if (rs[cur[k]].hi[axis] >= split) nxt.push_back(cur[k]);
-            if (nxt.size() >= (1ull << 32) || !budget->charge(2, 0)) return RT_ERR_OOM;
+            if (nxt.size() >= (1ull << 32)) return RT_ERR_OOM;
+            lvl_nodes += 2;
             nitems.push_back(Item{child, lb, hb});
             nitems.push_back(Item{child + 1, hb, (uint32_t)nxt.size()});
             out->nodes.emplace_back();
             out->nodes.emplace_back();
         }
+        if (!budget->charge(lvl_nodes, lvl_refs)) return RT_ERR_OOM;
         cur.swap(nxt);
         items.swap(nitems);
     }
