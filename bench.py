@@ -327,7 +327,8 @@ def run_config(name, cpu, build_id, per_batch_calls=True):
     w, h = int(loaded.info.width), int(loaded.info.height)
     tiles = [(0, 0, w, h)]
     nb = total // batch
-    group = max(1, min(nb, GROUP_ITEMS // (w * h * batch)))
+    group_items = int(os.environ.get("RT_DEBUG_GROUP_ITEMS") or GROUP_ITEMS)  # as rt_render_to_target reads it
+    group = max(1, min(nb, group_items // (w * h * batch)))
     res = {"workload": f"{scene}.yml {w}x{h}, {total} spp in batches of {batch}, kd_tree_depth "
                        f"{int(loaded.info.kd_tree_depth)}; {nb} batches per run, each batch's frame in its own "
                        f"device buffer, traced {group} batches per launch"}
