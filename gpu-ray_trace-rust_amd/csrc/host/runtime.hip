@@ -106,6 +106,7 @@ struct rt_ctx {
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
     uint4* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
     uint32_t pix_block = 1;           // RT_DEBUG_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
+    uint32_t pix_order = 0;           // RT_DEBUG_PIX_ORDER (experiment): 0 raster, 1 reverse, 2 centre first
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
     float4* d_out = nullptr;
@@ -711,6 +712,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.packet = 1u;
     if (const char* e = debug_env("PACKET")) d.packet = std::strcmp(e, "0") ? 1u : 0u;
     c->pix_block = RT_PIX_BLOCK;
+    if (const char* e = debug_env("PIX_ORDER")) c->pix_order = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = debug_env("PIX_BLOCK")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->pix_block = (uint32_t)v;
@@ -889,6 +891,30 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                                 const uint64_t key = rt_rng_pixel_key(c->sc.seed, fy * c->sc.width + fx);
                                 pq.push_back(make_uint4(pm[o], o, (uint32_t)key, (uint32_t)(key >> 32)));
                             }
+            if (c->pix_order && B > 1) {  // experiment: the same blocks in another order
+                const size_t bs = (size_t)B * B;
+                std::vector<std::pair<double, size_t>> key;  // (sort key, first entry of the block)
+                for (size_t b0 = 0; b0 < pq.size();) {
+                    const uint32_t xy = pq[b0].x;
+                    size_t b1 = b0 + 1;  // a block's entries share (x / B, y / B) and its tile
+                    while (b1 < pq.size() && b1 - b0 < bs && (pq[b1].x & 0xffffu) / B == (xy & 0xffffu) / B &&
+                           (pq[b1].x >> 16) / B == (xy >> 16) / B)
+                        ++b1;
+                    const double dx = (double)(xy & 0xffffu) - 0.5 * c->sc.width, dy = (double)(xy >> 16) - 0.5 * c->sc.height;
+                    key.push_back({c->pix_order == 1 ? -(double)b0 : dx * dx + dy * dy, b0});
+                    b0 = b1;
+                }
+                std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+                std::vector<uint4> re;
+                re.reserve(pq.size());
+                for (const auto& k : key) {
+                    const uint32_t xy = pq[k.second].x;
+                    for (size_t i = k.second; i < pq.size() && i - k.second < bs && (pq[i].x & 0xffffu) / B == (xy & 0xffffu) / B &&
+                                              (pq[i].x >> 16) / B == (xy >> 16) / B; ++i)
+                        re.push_back(pq[i]);
+                }
+                pq.swap(re);
+            }
             if (pix > c->d_pixmap_cap) {
                 if (c->d_pixmap) (void)hipFree(c->d_pixmap);
                 if (c->d_pixq) (void)hipFree(c->d_pixq);
