@@ -455,7 +455,8 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
     """Camera-ray packets (closest_packet: scalar-loaded nodes and leaf refs, per-lane
     near / far / push on the lane's own interval, deferred lanes, kd-restart from the packet's
     restart node, hand-over to the cooperative search), the cooperative search alone
-    (RT_DEBUG_PACKET=0) and the row-order queue (RT_DEBUG_PIX_BLOCK=1) each render the forward oracle's image
+    (RT_DEBUG_PACKET=0), the row-order queue (RT_DEBUG_PIX_BLOCK=1) and the queue's blocks in
+    reverse or centre-first order (RT_DEBUG_PIX_ORDER=1/2) each render the forward oracle's image
     (kdtree.rs:66-104), bit for bit, on two tiles and a full frame."""
     from rt_amd import render
 
@@ -464,9 +465,10 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
     o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
     o_full = oracle.render(sc, [(0, 0, w, h)], 0, 2 * spp, accum=oracle.ACCUM_FORWARD)
-    for cfg in (("1", "8"), ("0", "1"), ("1", "1"), ("0", "8")):
+    for cfg in (("1", "8", "0"), ("0", "1", "0"), ("1", "1", "0"), ("0", "8", "0"), ("1", "8", "1"), ("1", "8", "2")):
         monkeypatch.setenv("RT_DEBUG_PACKET", cfg[0])
         monkeypatch.setenv("RT_DEBUG_PIX_BLOCK", cfg[1])
+        monkeypatch.setenv("RT_DEBUG_PIX_ORDER", cfg[2])
         with render.Context(sc) as c:
             got = c.render(tiles, 0, spp)
         assert np.array_equal(got, o_tiles), (cfg, parity.stats(got, o_tiles))
