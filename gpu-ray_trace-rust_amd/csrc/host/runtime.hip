@@ -42,8 +42,8 @@ static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 // (its last paths finish on a few lanes), and only the folds, which update the shared
 // accumulators and the output, are chained in order by events.  A mesh launch's drain tail is
 // ~8-10 ms; a 1-spp a380 launch holds ~2 ms of work, so small launches (up to 2^21 samples) need
-// many of them in flight to cover one tail, larger ones 2 slots (biplane at 10 spp 590 / 587 /
-// 569 with 2 / 3 / 4).  The slots' streams overlap only on separate hardware queues: HIP maps
+// many of them in flight to cover one tail, larger ones fewer (mid_slots_for; round 2, biplane at
+// 10 spp: 590 / 587 / 569 with 2 / 3 / 4).  The slots' streams overlap only on separate hardware queues: HIP maps
 // streams onto GPU_MAX_HW_QUEUES queues (4 by default) as they are created, and streams sharing
 // a queue run in order (a380 at 1 spp: 4 queues 187 Msamples/s whatever the slots; 8 queues with
 // 2 / 4 / 6 slots 137 / 229 / 272; 12 queues, 8 slots 288-356).  So a context creates a slot's
@@ -66,6 +66,12 @@ static uint32_t slots_for_queues(int hw_queues) {
     return s < 2 ? 2u : (s > 12 ? 12u : (uint32_t)s);
 }
 static uint32_t small_grid_div(uint32_t slots) { return slots >= 12 ? 8u : (slots >= 8 ? 4u : 1u); }
+// Mid-size overlapped launches (2^21 .. 2^23 samples): half the small-launch slots, at most 6 (round
+// 4: a380's 10-batch launches of 7.2 M samples, 16 queues: 2 / 4 / 6 / 8 slots 400 / 421 / 426 /
+// 426 Msamples/s; at 4 queues 2 slots stay, where 4 ran -8.5%).  Larger ones keep 2 (biplane's
+// 14.4 M-sample launches: 6 slots -1.1%).
+static uint32_t mid_slots_for(uint32_t small_slots) { return std::max(2u, std::min(6u, small_slots / 2)); }
+constexpr uint64_t MID_LAUNCH_ITEMS = 1ull << 23;
 constexpr uint64_t SMALL_LAUNCH_ITEMS = 1ull << 21;  // default of rt_ctx::small_items
 struct Slot {
     hipStream_t stream = nullptr;
@@ -121,6 +127,7 @@ struct rt_ctx {
     uint64_t overlap_max_items = 1ull << 27;  // ... when it has at most this many samples
     uint32_t n_slots = 0;         // RT_DEBUG_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
     uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
+    uint32_t mid_slots = 2;       // slots of larger overlapped launches (mid_slots_for)
     uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_DEBUG_SMALL_LAUNCH_ITEMS: launches this size or less are small
     uint32_t grid_div = 0;        // RT_DEBUG_GRID_DIV; 0: small_grid_div(the launch's slots)
     uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_DEBUG_QUEUE_SHARDS)
@@ -736,6 +743,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const char* q = std::getenv("GPU_MAX_HW_QUEUES");  // what HIP read when it started
         const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
         c->small_slots = slots_for_queues(hwq);
+        c->mid_slots = mid_slots_for(c->small_slots);
     }
     if (const char* e = debug_env("QUEUE_SHARDS")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
@@ -1048,7 +1056,8 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
                 return set_err(c, RT_ERR_HIP, std::string("hipEventQuery(last fold): ") + hipGetErrorString(q));
             }
         }
-        const uint32_t n_slots = c->n_slots ? c->n_slots : (small ? c->small_slots : 2u);
+        const uint32_t n_slots = c->n_slots ? c->n_slots
+                                            : (small ? c->small_slots : (a.n_items <= MID_LAUNCH_ITEMS ? c->mid_slots : 2u));
         // the grid share follows the slots this launch rotates over (RT_DEBUG_GRID_DIV overrides)
         const uint32_t grid_div = c->grid_div ? c->grid_div : small_grid_div(n_slots);
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
@@ -1380,7 +1389,10 @@ extern "C" int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* 
     const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_batch, group_items / per_batch));
     // groups in flight beyond the one being read back: a small group launch rotates over the
     // small-launch slots, a larger one over two
-    const uint32_t ahead = (c->n_slots ? c->n_slots : (per_batch * G <= c->small_items ? c->small_slots : 2u)) - 1u;
+    const uint64_t gitems = per_batch * G;
+    const uint32_t ahead = (c->n_slots ? c->n_slots
+                                       : (gitems <= c->small_items ? c->small_slots
+                                                                   : (gitems <= MID_LAUNCH_ITEMS ? c->mid_slots : 2u))) - 1u;
     const uint32_t ring = (uint32_t)std::min<uint64_t>(n_batch, (uint64_t)G * (ahead + 1));
     std::vector<float4*> dbuf;
     std::vector<hipEvent_t> done;
