@@ -128,6 +128,7 @@ struct rt_ctx {
     uint32_t n_slots = 0;         // RT_DEBUG_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
     uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
     uint32_t mid_slots = 2;       // slots of larger overlapped launches (mid_slots_for)
+    uint32_t small_div = 0;       // grid share of a small launch behind a busy pipeline (0: small_grid_div)
     uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_DEBUG_SMALL_LAUNCH_ITEMS: launches this size or less are small
     uint32_t grid_div = 0;        // RT_DEBUG_GRID_DIV; 0: small_grid_div(the launch's slots)
     uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_DEBUG_QUEUE_SHARDS)
@@ -744,6 +745,15 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
         c->small_slots = slots_for_queues(hwq);
         c->mid_slots = mid_slots_for(c->small_slots);
+        // A tiny scene (queue_shards > 1, items of ~24 us) runs its launches of up to 2^24 samples
+        // on the small-launch pipeline (above), with the mid-size slot count and half the grid each
+        // (round 4, triangles.yml's 7.2 M-sample launches at 16 queues: 12 slots with an eighth of
+        // the grid 16,000 Msamples/s, 4 / 6 slots with a half 17,100 / 17,000, 2 slots with the full
+        // grid 16,700).
+        if (c->queue_shards > 1) {
+            c->small_slots = c->mid_slots;
+            if (c->small_slots >= 4) c->small_div = 2;
+        }
     }
     if (const char* e = debug_env("QUEUE_SHARDS")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
@@ -1059,7 +1069,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         const uint32_t n_slots = c->n_slots ? c->n_slots
                                             : (small ? c->small_slots : (a.n_items <= MID_LAUNCH_ITEMS ? c->mid_slots : 2u));
         // the grid share follows the slots this launch rotates over (RT_DEBUG_GRID_DIV overrides)
-        const uint32_t grid_div = c->grid_div ? c->grid_div : small_grid_div(n_slots);
+        const uint32_t grid_div = c->grid_div ? c->grid_div : (c->small_div ? c->small_div : small_grid_div(n_slots));
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
         for (uint32_t k = 0; k < (overlap ? n_slots : 1u); ++k) {
             const int e = ensure_slot(c, overlap ? k : c->cur_slot);
