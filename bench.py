@@ -10,7 +10,9 @@ gather; the default), or after every step (`--gather step`, the reference's per-
 read-back); the line reports the other mode beside the headline (rt_amd/shard.py FrameSteps).
 `value_host_inclusive` adds one D2H copy of the final frame to the timed steps (SURVEY.md §8d:
 "to final result on host"); `value` is the device-resident rate.  `bench_schema` 4: `value` is
-strong scaling (since round 3) and `weak` always holds the weak-scaling figure (N = 1: the same).  Inputs (scene, KD tree)
+strong scaling (since round 3) and `weak` always holds the weak-scaling figure (N = 1: the same);
+the N = 1 line ends with `configs_summary`, every config's value, CPU rate and bound in one short
+object (the line's tail alone shows them).  Inputs (scene, KD tree)
 are resident in HBM before the timed region.  N GPUs: one process per GPU
 (torch.distributed.run), image rows dealt to ranks as stripes of up to 8 rows, round-robin
 (rt_amd.shard.stripe_rows).
@@ -593,6 +595,18 @@ def main():
             res["configs"][name] = run_config(name, not args.no_cpu, build_id)
         # config 2 as a caller that leaves HIP's default of 4 hardware queues gets it
         res["configs"]["a380"]["hw_queues_4"] = config_at_queues("a380", 4)
+        # the configs' headline numbers once more, compactly, as the line's last key: a reader of
+        # only the line's tail still sees every config's value
+        res["configs_summary"] = {n: {"value": c.get("value"), "value_host_inclusive": c.get("value_host_inclusive"),
+                                      "cpu": (c.get("cpu_baseline") or {}).get("value"),
+                                      "bound": (c.get("roofline") or {}).get("bound"),
+                                      "frac": (c.get("roofline") or {}).get("frac")}
+                                  for n, c in res["configs"].items()}
+        res["configs_summary"]["a380"]["value_at_4_hw_queues"] = res["configs"]["a380"]["hw_queues_4"].get("value")
+        res["configs_summary"]["walled"] = {"value": res["value"], "value_host_inclusive": res.get("value_host_inclusive"),
+                                            "cpu": (res.get("cpu_baseline") or {}).get("value"),
+                                            "bound": (res.get("roofline") or {}).get("bound"),
+                                            "frac": (res.get("roofline") or {}).get("frac")}
     if dist:
         dist.destroy_process_group()
     if rank == 0:
