@@ -1,7 +1,7 @@
 // stub_hip.cpp — a host-only stand-in for the HIP runtime entry points librt_amd.so imports, for
 // CPU tests of the runtime's host logic (tests/test_runtime_stub.py).  LD_PRELOADed, it answers
 // every call the library makes: one "gfx950" device, host memory for device allocations, streams
-// and events as tokens, kernel launches counted and not run.  hipEventQuery answers what
+// and events as tokens, kernel launches logged (block, grid, stream) and not run.  hipEventQuery answers what
 // stub_hip_set_query() chose, so a test can make the launch pipeline see a failed earlier launch.
 // Test infrastructure only: never on the GPU box, never linked into the product.
 #include <hip/hip_runtime_api.h>
@@ -14,6 +14,8 @@ thread_local hipError_t g_last = hipSuccess;
 hipError_t g_query = hipSuccess;
 int g_launches = 0;
 int g_log[4096];  // block size of every launch, in order (128: a trace kernel, 256: the fold)
+int g_log_stream[4096];  // the launch's stream: its token number (streams are numbered as created)
+int g_log_grid[4096];    // the launch's workgroups
 int g_tokens[1024];
 int g_next_token = 0;
 dim3 g_grid, g_block;
@@ -34,6 +36,11 @@ int stub_hip_launches(void) { return g_launches; }
 int stub_hip_launch_log(int* out, int n) {
     const int m = g_launches < 4096 ? g_launches : 4096;
     for (int i = 0; i < m && i < n; ++i) out[i] = g_log[i];
+    return m;
+}
+int stub_hip_launch_detail(int* stream, int* grid, int n) {
+    const int m = g_launches < 4096 ? g_launches : 4096;
+    for (int i = 0; i < m && i < n; ++i) stream[i] = g_log_stream[i], grid[i] = g_log_grid[i];
     return m;
 }
 
@@ -79,8 +86,12 @@ const char* hipGetErrorString(hipError_t e) {
     return e == hipErrorLaunchFailure ? "stub: unspecified launch failure" : "stub error";
 }
 hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, const void*, int, size_t) { *n = 16; return hipSuccess; }
-hipError_t hipLaunchKernel(const void*, dim3, dim3 block, void**, size_t, hipStream_t) {
-    if (g_launches < 4096) g_log[g_launches] = (int)block.x;
+hipError_t hipLaunchKernel(const void*, dim3 grid, dim3 block, void**, size_t, hipStream_t s) {
+    if (g_launches < 4096) {
+        g_log[g_launches] = (int)block.x;
+        g_log_stream[g_launches] = s ? (int)(static_cast<int*>(static_cast<void*>(s)) - g_tokens) : -1;
+        g_log_grid[g_launches] = (int)grid.x;
+    }
     ++g_launches;
     return hipSuccess;
 }
