@@ -55,6 +55,60 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
 
+
+def self_launch_cmd(argv, env, port):
+    """The child command that runs `bench.py --gpus N` (N > 1) as N ranks when no launcher started
+    this process (WORLD_SIZE unset): torch.distributed.run on one node, ranks on 127.0.0.1, the
+    same arguments.  None when this process is already a rank, runs one GPU, or is bench's own
+    single-process child (--config-only) or rehearsal (--as-rank)."""
+    import argparse
+
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config-only", default=None)
+    ap.add_argument("--as-rank", default=None)
+    known, _ = ap.parse_known_args(argv)
+    if "WORLD_SIZE" in env or known.gpus <= 1 or known.config_only or known.as_rank:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(known.gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def self_launch(argv):
+    """Runs self_launch_cmd's ranks as a CHILD process (subprocess: fork + exec in the child, before
+    this process touches the GPU; never an exec of this process), streams the ranks' output, and
+    prints rank 0's JSON line as this process's one stdout line.  Returns the exit code, or None
+    when no launch is needed."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = self_launch_cmd(argv, os.environ, port)
+    if cmd is None:
+        return None
+    env = dict(os.environ, RT_BENCH_LAUNCHER="bench.py")
+    print("bench.py: --gpus > 1 without a launcher: starting " + " ".join(cmd), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    lines = []
+    for ln in p.stdout:
+        if ln.startswith("{"):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    if lines:
+        print(lines[-1], flush=True)
+    return rc if (rc or lines) else 1
+
+
+if __name__ == "__main__" and os.environ.get("WORLD_SIZE") is None:
+    _rc = self_launch(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
 # The launch pipeline's slots each want their own HIP hardware queue (DESIGN.md §5, launch
 # pipeline): this benchmark chooses GPU_MAX_HW_QUEUES = 16 before HIP starts unless the caller
 # asked for at least that, and reports what it ran with (rt_amd itself keeps explicit values).
@@ -63,7 +117,10 @@ try:
     _q = int(HW_QUEUES_BEFORE or "0")
 except ValueError:
     _q = 0
-if _q < 16 and "--config-only" not in sys.argv:  # config_at_queues' child keeps the value it was given
+# config_at_queues' child keeps the value it was given, and so do same-device test ranks (several
+# processes sharing one GPU's hardware queues)
+_keep = "--config-only" in sys.argv or ("--same-device" in sys.argv and HW_QUEUES_BEFORE is not None)
+if _q < 16 and not _keep:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import rt_amd  # noqa: E402
 
@@ -250,6 +307,10 @@ def cpu_baseline(loaded, spp, threads=None, reps=3, rows_step=1):
         return t1 - t0, (c1.user - c0.user) + (c1.system - c0.system)
 
     timed(0)  # one-time loading
+    # one untimed call at the measured spp: the first render call of a process ran at a third of
+    # the later ones (round 4, triangles: 35.5 / 112.3 / 111.6 Msamples/s; thread pool and page
+    # warm-up), which the median hid but the spread showed
+    timed(spp)
     t_build = min(timed(0)[0], timed(0)[0])
     runs = []
     for _ in range(reps):
@@ -277,7 +338,8 @@ def cpu_baseline(loaded, spp, threads=None, reps=3, rows_step=1):
             "runs": [{k: round(v, 3) for k, v in r.items()} for r in runs],
             "threads": threads, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "cpu_model": model,
             "kd_build_s": round(t_build, 3),
-            "sample": f"{what}, {spp} spp (BASELINE.md §2), {reps} calls on {threads} threads, median "
+            "sample": f"{what}, {spp} spp (BASELINE.md §2), one untimed warm-up call at that spp, then {reps} calls on "
+                      f"{threads} threads, median "
                       f"(KD build timed apart, CPU quota {quota or 'none'}); oracle/oracle.cpp recursive radiance; "
                       f"effective_cores = process CPU-seconds / wall-seconds of each call"}
 
@@ -434,6 +496,9 @@ def main():
                     help="gloo: gather host copies (multi-rank test with every rank on one GPU)")
     ap.add_argument("--same-device", action="store_true", help="every rank on device 0 (tests; gloo only)")
     ap.add_argument("--dump-frame", default=None, help="rank 0 saves the last assembled frame (.npy)")
+    ap.add_argument("--frame-digest", action="store_true",
+                    help="rank 0 adds the sha256 of every run's assembled frame (headline, other gather mode, "
+                         "weak / strong) to the line: bit-equality checks of large frames without dumping them")
     ap.add_argument("--gather", default="frame", choices=("frame", "step"),
                     help="N > 1: gather the ranks' tiles once at frame end (north_star; default) or after every "
                          "step (the reference's per-batch read-back); the other mode is reported beside it")
@@ -493,11 +558,22 @@ def main():
                  value_host_inclusive=job_samples * args.steps / (r["elapsed_s"] + r["host_copy_s"]) / 1e6)
         return fs, r
 
+    def digest(fs):
+        """rank 0: sha256 of the assembled frame's bytes (None elsewhere / when not asked)."""
+        if not args.frame_digest or args.as_rank or rank != 0:
+            return None
+        import hashlib
+
+        import numpy as np
+
+        return hashlib.sha256(np.ascontiguousarray(fs.frame(), dtype=np.float32).tobytes()).hexdigest()
+
     fs, r = timed_run(strong, args.gather)
     elapsed, ls, spp_rank, npix = r["elapsed_s"], r["launch"], r["spp_rank"], r["npix"]
     # after the timed region: rank 0 reassembles the last gathered frame and checks that every
     # pixel was rendered by some rank (alpha is 1 exactly where written)
     frame_complete = None
+    frame_sha = digest(fs)
     if not args.as_rank and rank == 0:
         frame = fs.frame()
         frame_complete = bool((frame[..., 3] == 1.0).all())
@@ -505,6 +581,7 @@ def main():
             import numpy as np
 
             np.save(args.dump_frame, frame)
+        del frame
     del fs
 
     n_launch = ls["n_trace_launches"]
@@ -524,6 +601,9 @@ def main():
                       "parallelism": f"tiles{world}", "dispatch": "sync" if args.sync else "async",
                       "dist_backend": args.dist_backend if world > 1 else None}}
     res["frame_complete"] = frame_complete
+    if frame_sha:
+        res["frame_sha256"] = frame_sha
+    res["launcher"] = (os.environ.get("RT_BENCH_LAUNCHER") or "torch.distributed.run") if world > 1 else None
     # the final frame on the host (SURVEY.md §8d "to final result on host"): one D2H copy of the
     # (gathered) frame after the timed steps, added to their time; `value` stays device-resident
     res["value_host_inclusive"] = round(r["value_host_inclusive"], 3)
@@ -543,16 +623,22 @@ def main():
     if world > 1:
         # the other gather mode (frame end <-> every step), same scaling as the headline
         other = "step" if args.gather == "frame" else "frame"
-        _, rg = timed_run(strong, other)
+        fg, rg = timed_run(strong, other)
         res[f"gather_{other}"] = {
             "value": round(rg["value"], 3), "ms_per_step": round(rg["elapsed_s"] / args.steps * 1e3, 3),
             "gathers": rg["gathers"], "ms_per_gather": round(rg.get("gather_ms_per_gather", 0.0), 3),
             "gather_ms_per_step": round(rg.get("gather_ms_per_step", 0.0), 3)}
+        if args.frame_digest and rank == 0:
+            res[f"gather_{other}"]["frame_sha256"] = digest(fg)
+        del fg
         # weak scaling beside the strong headline (each rank keeps the 1-GPU step's work)
-        _, rw = timed_run(not strong, args.gather)
+        fw, rw = timed_run(not strong, args.gather)
         res["weak" if strong else "strong"] = {
             "value": round(rw["value"], 3), "ms_per_step": round(rw["elapsed_s"] / args.steps * 1e3, 3),
             "spp_per_rank_step": rw["spp_rank"], "gather_ms_per_step": round(rw.get("gather_ms_per_step", 0.0), 3)}
+        if args.frame_digest and rank == 0:
+            res["weak" if strong else "strong"]["frame_sha256"] = digest(fw)
+        del fw
     elif not args.as_rank:
         res["weak"] = {"value": res["value"], "note": "N = 1: weak and strong scaling are the same run"}
 

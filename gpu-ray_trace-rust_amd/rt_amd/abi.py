@@ -116,6 +116,12 @@ class rt_work_counts(C.Structure):
                                            "tri_tests", "hits", "mesh_hits")]
 
 
+class rt_frame_stats(C.Structure):
+    _fields_ = [("render_ms_max", C.c_float), ("peer_copy_ms_max", C.c_float), ("place_ms", C.c_float),
+                ("n_parts", C.c_uint32), ("stripe_rows", C.c_uint32), ("n_gathers", C.c_uint32),
+                ("n_peer_copies", C.c_uint32)]
+
+
 RT_SCHEME_YAML, RT_SCHEME_JSON = 0, 1
 
 
@@ -157,6 +163,24 @@ EXPORTS = {
     "rt_render_to_target": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(rt_camera),
                                       C.POINTER(rt_render_info), C.c_uint32, C.c_uint32, C.c_int,
                                       C.POINTER(C.c_uint8), C.c_void_p, C.c_void_p]),
+    "rt_stripe_rows": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+    "rt_stripe_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.POINTER(rt_tile), C.c_uint32, C.POINTER(C.c_uint32)]),
+    "rt_frame_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(rt_camera), C.POINTER(rt_render_info),
+                                  C.POINTER(rt_kd_tree), C.POINTER(C.c_int), C.c_uint32, C.c_uint32,
+                                  C.POINTER(C.c_void_p)]),
+    "rt_frame_render": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32]),
+    "rt_frame_gather": (C.c_int, [C.c_void_p, P_f, C.c_void_p]),
+    "rt_frame_synchronize": (C.c_int, [C.c_void_p]),
+    "rt_frame_get_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_frame_stats)]),
+    "rt_frame_part": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int), C.POINTER(C.c_void_p),
+                                C.POINTER(C.c_uint32)]),
+    "rt_frame_last_error": (C.c_char_p, [C.c_void_p]),
+    "rt_frame_destroy": (C.c_int, [C.c_void_p]),
+    "rt_render_to_target_devices": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(rt_camera),
+                                              C.POINTER(rt_render_info), C.c_uint32, C.c_uint32,
+                                              C.POINTER(C.c_int), C.c_uint32, C.POINTER(C.c_uint8), C.c_void_p,
+                                              C.c_void_p]),
     "rt_scheme_load": (C.c_int, [C.c_char_p, C.c_uint64, C.c_uint32, C.c_char_p, C.c_uint64,
                                  C.POINTER(C.c_void_p)]),
     "rt_scheme_view_get": (C.c_int, [C.c_void_p, C.POINTER(rt_scheme_view)]),

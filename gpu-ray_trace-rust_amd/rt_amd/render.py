@@ -203,6 +203,81 @@ class Context:
             pass
 
 
+def stripe_tiles(width: int, height: int, index: int, n_parts: int, stripe: int = 0, lib=None) -> list:
+    """Context `index`'s tiles of the library's stripe deal (rt_stripe_tiles; stripe 0: the
+    library's rt_stripe_rows), as (x0, y0, w, h) tuples."""
+    lib = lib or abi.load_library()
+    n = C.c_uint32()
+    abi.check(lib, lib.rt_stripe_tiles(width, height, stripe, index, n_parts, None, 0, C.byref(n)))
+    arr = (abi.rt_tile * max(n.value, 1))()
+    abi.check(lib, lib.rt_stripe_tiles(width, height, stripe, index, n_parts, arr, n.value, C.byref(n)))
+    return [(t.x0, t.y0, t.w, t.h) for t in arr[:n.value]]
+
+
+class Frame:
+    """One frame over several contexts (rt_frame_*): each renders its stripes on its device, one
+    gather per frame assembles the frame on devices[0] (SURVEY.md §8e at the C ABI)."""
+
+    def __init__(self, loaded: LoadedScheme, devices, stripe: int = 0, lib=None,
+                 tree: "abi.rt_kd_tree | None" = None):
+        self.lib = lib or abi.load_library()
+        self.loaded = loaded
+        self.devices = [int(d) for d in devices]
+        self.ptr = C.c_void_p()
+        devs = (C.c_int * len(self.devices))(*self.devices)
+        st = self.lib.rt_frame_create(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info),
+                                      C.byref(tree) if tree is not None else None, devs, len(self.devices),
+                                      int(stripe), C.byref(self.ptr))
+        abi.check(self.lib, st)
+
+    def _check(self, st):
+        if st != abi.RT_OK:
+            msg = abi.load_library().rt_status_string(st).decode()
+            raise abi.RtError(st, msg + " — " + (self.lib.rt_frame_last_error(self.ptr) or b"").decode())
+
+    def render(self, sample_begin: int, sample_count: int):
+        """Every context advances its stripes by [sample_begin, sample_begin + count) (enqueued)."""
+        self._check(self.lib.rt_frame_render(self.ptr, int(sample_begin), int(sample_count)))
+
+    def gather(self, want_host: bool = True, dev_ptr: int = 0) -> np.ndarray | None:
+        """The frame-end gather; the frame (H, W, 4) f32 on the host when want_host."""
+        w, h = int(self.loaded.info.width), int(self.loaded.info.height)
+        out = np.empty((h, w, 4), dtype=np.float32) if want_host else None
+        self._check(self.lib.rt_frame_gather(self.ptr, out.ctypes.data_as(abi.P_f) if want_host else None,
+                                             C.c_void_p(dev_ptr or None)))
+        return out
+
+    def synchronize(self):
+        self._check(self.lib.rt_frame_synchronize(self.ptr))
+
+    def stats(self) -> dict:
+        s = abi.rt_frame_stats()
+        self._check(self.lib.rt_frame_get_stats(self.ptr, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in abi.rt_frame_stats._fields_}
+
+    def part(self, index: int) -> dict:
+        dev, ctx, nt = C.c_int(), C.c_void_p(), C.c_uint32()
+        self._check(self.lib.rt_frame_part(self.ptr, index, C.byref(dev), C.byref(ctx), C.byref(nt)))
+        return {"device": dev.value, "ctx": ctx, "n_tiles": nt.value}
+
+    def close(self):
+        if self.ptr:
+            self.lib.rt_frame_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def rgba_to_u8(rgba: np.ndarray, lib=None) -> np.ndarray:
     """rgb_f_to_u8 (draw_scene.rs:104-108) through the C++ host."""
     lib = lib or abi.load_library()
@@ -224,5 +299,21 @@ def render_to_target(loaded: LoadedScheme, spp: int, batch: int, device: int = 0
     st = lib.rt_render_to_target(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info), int(spp),
                                  int(batch), int(device), target.ctypes.data_as(C.POINTER(C.c_uint8)),
                                  C.cast(cb, C.c_void_p) if cb else None, None)
+    abi.check(lib, st)
+    return target
+
+
+def render_to_target_devices(loaded: LoadedScheme, spp: int, batch: int, devices, update_hook=None,
+                             lib=None) -> np.ndarray:
+    """render_to_target_gpu over several contexts (rt_render_to_target_devices)."""
+    lib = lib or abi.load_library()
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    target = np.zeros((h, w, 4), dtype=np.uint8)
+    HOOK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32)
+    cb = HOOK(lambda _u, done: update_hook(target, int(done))) if update_hook else None
+    devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+    st = lib.rt_render_to_target_devices(C.byref(loaded.desc), C.byref(loaded.cam), C.byref(loaded.info), int(spp),
+                                         int(batch), devs, len(devices), target.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                         C.cast(cb, C.c_void_p) if cb else None, None)
     abi.check(lib, st)
     return target

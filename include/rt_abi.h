@@ -321,6 +321,61 @@ int rt_render_to_target(const rt_scene_desc* scene, const rt_camera* cam,
                         const rt_render_info* info, uint32_t spp, uint32_t batch,
                         int device, uint8_t* target, rt_update_hook hook, void* user);
 
+/* ------------------------------------------- one frame over several devices */
+/* New: the reference is single-adapter (gpu_utils.rs:614-637).  The frame's rows are dealt to
+ * n contexts as stripes of `stripe_rows` rows, round-robin (stripe i to context i % n; consecutive
+ * stripes of one context merge into one tile); every context renders its stripes for the whole
+ * sample range on its device, and ONE gather per frame assembles the frame on devices[0]: a
+ * context on another device copies its tile radiance there over xGMI (peer copy), then each
+ * context's stripes are placed by one strided copy.  A device ordinal may repeat (several contexts
+ * on one device).  The frame equals a one-context frame bit for bit (the RNG and the running mean
+ * are keyed on the global pixel and the absolute sample).  The caller is the reference's render
+ * thread (renderer.rs:43-60 -> render_to_target_gpu, draw_scene.rs:17-47): no torch, no launcher. */
+typedef struct rt_frame rt_frame;
+
+/* The tallest stripe S <= 8 rows with height % (S * n_parts) == 0 (equal stripe counts), else 1. */
+uint32_t rt_stripe_rows(uint32_t height, uint32_t n_parts);
+/* Context `index`'s tiles (x0 = 0, full-width row ranges) of the stripe deal; stripe_rows 0 picks
+ * rt_stripe_rows.  *n_tiles is the count; at most `cap` tiles are written (tiles may be NULL). */
+int rt_stripe_tiles(uint32_t width, uint32_t height, uint32_t stripe_rows, uint32_t index, uint32_t n_parts,
+                    rt_tile* tiles, uint32_t cap, uint32_t* n_tiles);
+
+/* One rt_ctx per entry of devices[] (created side by side, one KD build shared: `tree` or built
+ * here), its stripe buffer, and the frame (width * height RGBA f32) on devices[0]. */
+int rt_frame_create(const rt_scene_desc* scene, const rt_camera* cam, const rt_render_info* info,
+                    const rt_kd_tree* tree, const int* devices, uint32_t n_devices, uint32_t stripe_rows,
+                    rt_frame** out);
+/* Every context advances its stripes over [sample_begin, sample_begin + sample_count) (the running
+ * mean of rt_render); enqueued on the devices, returns at once.  Split calls equal one call. */
+int rt_frame_render(rt_frame* frame, uint64_t sample_begin, uint32_t sample_count);
+/* The frame-end gather: waits for the enqueued renders, assembles the frame on devices[0] and copies
+ * it to out_rgba (host, width * height * 4 floats) and / or out_rgba_device (devices[0] memory);
+ * either may be NULL.  Synchronous. */
+int rt_frame_gather(rt_frame* frame, float* out_rgba, float* out_rgba_device);
+/* Waits for everything enqueued on every context and closes their timing windows. */
+int rt_frame_synchronize(rt_frame* frame);
+typedef struct rt_frame_stats {
+    float    render_ms_max;      /* the slowest context's device window (rt_last_kernel_ms) */
+    float    peer_copy_ms_max;   /* the slowest peer copy of the last gather (0: one device) */
+    float    place_ms;           /* the last gather's placement on devices[0] */
+    uint32_t n_parts, stripe_rows;
+    uint32_t n_gathers;          /* gathers since rt_frame_create */
+    uint32_t n_peer_copies;      /* peer copies since rt_frame_create */
+} rt_frame_stats;
+int rt_frame_get_stats(rt_frame* frame, rt_frame_stats* out);   /* synchronizes first */
+/* Context `index`: its device, its rt_ctx (owned by the frame: do not destroy) and tile count. */
+int rt_frame_part(const rt_frame* frame, uint32_t index, int* device, rt_ctx** ctx, uint32_t* n_tiles);
+const char* rt_frame_last_error(const rt_frame* frame);
+int rt_frame_destroy(rt_frame* frame);
+
+/* render_to_target_gpu (draw_scene.rs:17-47) over several devices: spp / batch batches, each
+ * rendered by every context on its stripes and gathered once; RGBA8 into `target` and
+ * hook(user, samples_done) after every batch, in order.  The targets equal rt_render_to_target's. */
+int rt_render_to_target_devices(const rt_scene_desc* scene, const rt_camera* cam,
+                                const rt_render_info* info, uint32_t spp, uint32_t batch,
+                                const int* devices, uint32_t n_devices, uint8_t* target,
+                                rt_update_hook hook, void* user);
+
 /* ------------------------------------------------------------ host: the boundary's caller */
 /* Scheme loading in C++ (what the reference's builder does before the `use_gpu` switch):
  * Scheme::from_yml + apply_corrections (builder/mod.rs:63-72), member conversion in renderable

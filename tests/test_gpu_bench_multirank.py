@@ -24,22 +24,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _bench(tmp_path, tag, world, extra):
-    dump = str(tmp_path / f"{tag}.npy")
-    args = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-roofline",
-            "--no-configs", "--dump-frame", dump] + extra
+def _bench(tmp_path, tag, world, extra, launcher=True, steps=2, warmup=1, dump=True, timeout=240, env_extra=None):
+    dump_path = str(tmp_path / f"{tag}.npy")
+    args = ["bench.py", "--gpus", str(world), "--steps", str(steps), "--warmup", str(warmup), "--no-cpu",
+            "--no-roofline", "--no-configs"] + (["--dump-frame", dump_path] if dump else []) + extra
     if world > 1:
+        args += ["--dist-backend", "gloo", "--same-device"]
+    if world > 1 and launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args + \
-              ["--dist-backend", "gloo", "--same-device"]
-    else:
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:  # one GPU, or N ranks started by bench.py itself (no launcher: the driver's plain command)
         cmd = [sys.executable] + args
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(line) == 1, r.stdout  # one JSON line, from rank 0 only
-    return json.loads(line[0]), np.load(dump)
+    return json.loads(line[0]), (np.load(dump_path) if dump else None)
 
 
 @pytest.mark.parametrize("scene,spp", [("walled", 8), ("biplane", 2)])
@@ -57,3 +60,33 @@ def test_bench_two_ranks_equal_one(gpu_available, tmp_path, scene, spp):
     one2, f12 = _bench(tmp_path, "one2", 1, ["--scene", scene, "--spp-per-step", str(2 * spp)])
     assert weak["scaling"] == "weak" and "strong" in weak
     assert np.array_equal(fw, f12)
+
+
+def test_bench_starts_its_own_ranks(gpu_available, tmp_path):
+    """`python bench.py --gpus 2` with no launcher (the driver's plain command line) starts the two
+    ranks itself (torch.distributed.run as a child) and prints rank 0's one line: n_gpus 2, the
+    frame complete and equal to one rank's bit for bit."""
+    one, f1 = _bench(tmp_path, "one", 1, ["--scene", "walled", "--spp-per-step", "8"])
+    two, f2 = _bench(tmp_path, "self", 2, ["--scene", "walled", "--spp-per-step", "8"], launcher=False)
+    assert two["n_gpus"] == 2 and two["frame_complete"] and two["launcher"] == "bench.py"
+    assert np.array_equal(f1, f2)
+
+
+def test_config5_eight_ranks_on_one_gpu(gpu_available, tmp_path):
+    """BASELINE config 5's exact split — spaceship_r1 at 4096 x 4096 over 8 ranks (8-row stripes, 64
+    per rank), the 8-way gather and rank 0's assembly — as bench.py runs it, with every rank on
+    device 0 (gloo), 1 spp per step, 2 steps: the strong headline (gather at frame end), the
+    per-step gather and the weak run (8 spp per rank-step) each equal the 1-rank frame of the same
+    samples bit for bit (sha256 of the assembled frames)."""
+    common = ["--scene", "spaceship_r1", "--width", "4096", "--height", "4096", "--frame-digest"]
+    q4 = {"GPU_MAX_HW_QUEUES": "4"}  # eight processes share one GPU's hardware queues
+    eight, _ = _bench(tmp_path, "eight", 8, common + ["--spp-per-step", "1"], launcher=False, warmup=0,
+                      dump=False, timeout=600, env_extra=q4)
+    one, _ = _bench(tmp_path, "one1", 1, common + ["--spp-per-step", "1"], warmup=0, dump=False)
+    one8, _ = _bench(tmp_path, "one8", 1, common + ["--spp-per-step", "8"], warmup=0, dump=False)
+    assert eight["n_gpus"] == 8 and eight["frame_complete"] and eight["config"]["stripes"] == "8-row round-robin"
+    assert eight["gather"]["gathers"] == 1  # the frame-end gather: once per frame
+    assert eight["frame_sha256"] == one["frame_sha256"]
+    assert eight["gather_step"]["frame_sha256"] == one["frame_sha256"]
+    assert eight["weak"]["spp_per_rank_step"] == 8
+    assert eight["weak"]["frame_sha256"] == one8["frame_sha256"]
