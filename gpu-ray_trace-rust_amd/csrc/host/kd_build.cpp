@@ -321,7 +321,7 @@ extern "C" int rt_kd_build(const rt_scene_desc* scene, uint32_t max_depth, rt_kd
         for (size_t e = 0; e < rs.size(); ++e)
             for (int a = 0; a < 3; ++a) cen[3 * e + a] = 0.5f * (rs[e].lo[a] + rs[e].hi[a]);
         // The top STOP levels are built here; the subtrees below them, independent of each other,
-        // on a few threads (RT_KD_THREADS, default up to 8; 1: all on this thread).  The merge
+        // on a few threads (RT_DEBUG_KD_THREADS, default up to 8; 1: all on this thread).  The merge
         // renumbers everything breadth first, so the tree is byte-identical either way.
         unsigned n_thr = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = std::getenv("RT_DEBUG_KD_THREADS")) n_thr = (unsigned)std::max(1, std::atoi(e));

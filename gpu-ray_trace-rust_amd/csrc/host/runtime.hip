@@ -168,8 +168,9 @@ static int guarded(rt_ctx* c, F f) {
 #define RT_PIX_BLOCK 8  // queue order of a launch's pixels: B x B blocks of each tile (1: row order)
 #endif
 
-// A/B and test knobs, read here and nowhere else, all named RT_DEBUG_<name> (INTEGRATION.md
-// lists them).  A caller needs none of them: each selects an alternative schedule or layout that
+// A/B and test knobs of the runtime, all named RT_DEBUG_<name> (INTEGRATION.md lists them), read
+// here; the host KD build reads its own two, RT_DEBUG_KD_THREADS and RT_DEBUG_KD_BUDGET
+// (kd_build.cpp).  A caller needs none of them: each selects an alternative schedule or layout that
 // the GPU tests check bit-invariant against the oracle.  The one other variable the library reads
 // is HIP's own GPU_MAX_HW_QUEUES (the hardware queues the launch pipeline can use).
 static const char* debug_env(const char* name) {
@@ -730,6 +731,22 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         const unsigned long v = std::strtoul(e, nullptr, 10);
         d.restart = v > 2 ? 1u : (uint32_t)v;
     }
+    // The pool kernel (trace.hip g_pool4): the general kernel with every leaf-testable primitive
+    // resident in LDS, stackless.  RT_DEBUG_POOL: 0 off, 768 / 1024 that many threads per workgroup
+    // (when the pool fits), "auto" 768 when keys + pool fit in half a CU's LDS (two workgroups per
+    // CU), else 1024 when they fit in the whole.
+    d.n_pool = scene->n_spheres + scene->n_free_tris + (uint32_t)mf.tris.size();
+    d.pool_nt = 0;
+    if (!d.spheres_only && !d.dls) {
+        const char* e = debug_env("POOL");
+        const std::string mode = e ? e : "0";
+        constexpr size_t LDS_CU = 160u * 1024u;
+        auto fits = [&](uint32_t nt, size_t budget) { return pool_lds_bytes(nt, d.n_pool) <= budget; };
+        if (mode == "auto") d.pool_nt = fits(768, LDS_CU / 2) ? 768u : (fits(1024, LDS_CU) ? 1024u : 0u);
+        else if (mode == "768" && fits(768, LDS_CU)) d.pool_nt = 768;
+        else if (mode == "1024" && fits(1024, LDS_CU)) d.pool_nt = 1024;
+        if (d.pool_nt) d.restart = 1;  // the pool kernel is stackless (its LDS holds no stack)
+    }
     // Overlapped launches pay off while a launch's drain tail is a sizeable share of it: mesh
     // launches (8-10 ms tails) and small sphere-only ones — walled's ~0.4 ms tail on
     // one rank's 90 M-sample share at N = 8 (9 ms): +3% overlapped, while at 180 M it is neutral
@@ -1027,7 +1044,8 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
     int per_cu = 0;  // the queue grid: the resident workgroups of this scene's kernel
     HIPCHK(c, queue_blocks_per_cu(a, &per_cu));
     if (per_cu < 1) per_cu = 1;
-    const uint64_t lanes = (uint64_t)c->n_cu * (uint64_t)per_cu * BLOCK;
+    const uint32_t tpb = queue_block_threads(a);  // threads per workgroup of the scene's queue kernel
+    const uint64_t lanes = (uint64_t)c->n_cu * (uint64_t)per_cu * tpb;
     // the counter overshoots n_items by at most one grab (<= 1024 = 16 x 64) per wave
     if (n_out * chunk + lanes * 16 >= (1ull << 32)) chunk = ((1ull << 32) - lanes * 16 - 1) / n_out;
     if (chunk < 1) return set_err(c, RT_ERR_INVALID_ARG, "too many pixels for one launch");
@@ -1085,7 +1103,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         a.queue = sl.queue;
         a.n_shards = c->queue_shards;
         a.gstack = nullptr;
-        if (const size_t gb = queue_gstack_bytes(a, (uint32_t)(lanes / BLOCK))) {
+        if (const size_t gb = queue_gstack_bytes(a, (uint32_t)(lanes / tpb))) {
             if (gb > sl.gstack_cap) {
                 HIPCHK(c, hipStreamSynchronize(sl.stream));
                 if (sl.gstack) (void)hipFree(sl.gstack);
@@ -1101,7 +1119,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         if (a.sample_count) {
             HIPCHK(c, hipMemsetAsync(sl.queue, 0, QUEUE_BYTES, sl.stream));
             if ((st = record_launch_event(c, true, sl.stream))) return st;
-            uint32_t nb = (uint32_t)(lanes / BLOCK);
+            uint32_t nb = (uint32_t)(lanes / tpb);
             if (overlap && small && busy && grid_div > 1)
                 nb = nb / grid_div > (uint32_t)c->n_cu ? nb / grid_div : (uint32_t)c->n_cu;
             HIPCHK(c, launch_trace_queue(a, nb, sl.stream));

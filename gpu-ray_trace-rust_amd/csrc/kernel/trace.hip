@@ -149,10 +149,12 @@ __device__ __forceinline__ V3 div3(V3 a, float b) {
     if (__builtin_expect(!(mk_range(b) && mk_num(a.x) && mk_num(a.y) && mk_num(a.z)), 0)) q = a / b;
     return q;
 }
-// sqrtf(x), bit for bit, for every x in [2^-80, FLT_MAX] (exhaustive, tools/check_exact_ops.hip;
-// below 2^-80, at 0 and at +inf it is not): Markstein's correction of s = x * rsq(x) with one
-// rounding, s + (x - s^2) * rsq(x) / 2 — five instructions instead of hipcc's IEEE sequence.
-__device__ __forceinline__ float sqrt_rn(float x) {
+// sqrtf(x), bit for bit, for every x in [2^-80, FLT_MAX] (exhaustive, tools/check_exact_ops.hip):
+// Markstein's correction of s = x * rsq(x) with one rounding, s + (x - s^2) * rsq(x) / 2 — five
+// instructions instead of hipcc's IEEE sequence.  DOMAIN: [2^-80, FLT_MAX] only — at +-0 and +inf
+// it returns NaN, below 2^-80 it is inexact.  A caller whose argument may leave that range goes
+// through sqrt_nonneg / sqrt_draw (the guarded forms below), as every current caller does.
+__device__ __forceinline__ float sqrt_rn_normal(float x) {
     const float y = __builtin_amdgcn_rsqf(x);
     const float s = x * y;
     return fmaf(fmaf(-s, s, x), 0.5f * y, s);
@@ -160,14 +162,14 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 // sqrtf(x) for x >= -0 (an fmaxf(y, 0), a dot(a, a), a uniform draw): one compare sends ±0,
 // (0, 2^-80), +inf and NaN to sqrtf — a divergent branch no lane normally takes.
 __device__ __forceinline__ float sqrt_nonneg(float x) {
-    float s = sqrt_rn(x);
+    float s = sqrt_rn_normal(x);
     if (__builtin_expect(__float_as_uint(x) - (47u << 23) >= 0x7f800000u - (47u << 23), 0)) s = sqrtf(x);
     return s;
 }
 // sqrtf of a uniform draw u or of 1 - u: 0 or in [2^-24, 1] (rt_rng.h's (x >> 8) * 2^-24,
-// u <= 1 - 2^-24), inside sqrt_rn's exact range but for 0.
+// u <= 1 - 2^-24), inside sqrt_rn_normal's exact range but for 0.
 __device__ __forceinline__ float sqrt_draw(float x) {
-    return x == 0.0f ? x : sqrt_rn(x);
+    return x == 0.0f ? x : sqrt_rn_normal(x);
 }
 // nalgebra normalize: a / |a| per component.  div3's guard, specialised: |a_i| < 2^60 follows
 // from |a| < 2^60 (|a_i| >= 2^60 makes fl(a.a) >= 2^120), so each numerator only needs to be
@@ -268,7 +270,7 @@ __device__ __forceinline__ bool sphere_roots(SphDisc q, float* l) {
     // thing2 <= 0 (or NaN) gives a NaN or 0 here, but then disc is false and *l is never used
     // sqrt_nonneg's tiny-input guard as one float compare beside disc (lanes without disc
     // never use the root, so only disc lanes with thing2 < 2^-80 need sqrtf)
-    float thing = sqrt_rn(q.thing2);
+    float thing = sqrt_rn_normal(q.thing2);
     if (__builtin_expect(disc && q.thing2 < 0x1p-80f, 0)) thing = sqrtf(q.thing2);
     const float l0 = offset + thing, l1 = offset - thing;
     *l = l1 > 0.0f ? l1 : l0;  // sphere.rs:95
@@ -723,6 +725,49 @@ struct PkScene {
 // win (see leaf_closest).  The owner then re-tests the winning ref for its barycentrics.
 __shared__ unsigned long long g_coop_key[BLOCK];
 
+// Whole-pool residency (the pool kernel, DevScene::pool_nt > 0).  A scene whose leaf-testable
+// primitives fit in LDS keeps all of them there for the whole launch, copied once per workgroup
+// at its start, so a cooperative pass reads a pair's primitive with ds_read instead of three 16-B
+// gathers through the vector-memory return path (TA / TD), which bounds the mesh kernels
+// (spaceship_r1: 44.5 of its 78.3 vector wave-loads per sample were those gathers).  Unlike the
+// per-round slabs of RT_DEBUG_KD_RESTART=2 nothing is copied again during the launch.  The pool
+// kernel's dynamic LDS: the workgroup's leaf-minimum keys (PNT x 8 B, coop_leaf's g_coop_key),
+// then the pool as three arrays, 36 B per primitive, the prim4 values without their padding:
+// A = {v0.xyz, e1.x}, B = {e1.yz, e2.xy}, C = e2.z; a sphere is A = {c, r}, B = C = 0.  PNT =
+// threads per workgroup: 768 (two workgroups per CU, 6 waves per SIMD, when keys and pool fit in
+// half the CU's 160 KiB) or 1024 (one per CU, 4 waves per SIMD).
+extern __shared__ float4 g_pool4[];
+template <int PNT>
+__device__ __forceinline__ unsigned long long* coop_keys() {
+    if constexpr (PNT > 0) return reinterpret_cast<unsigned long long*>(g_pool4);
+    else return g_coop_key;
+}
+template <int PNT>
+__device__ __forceinline__ void pool_load(uint32_t n, uint32_t i, float4& a0, float4& a1, float4& a2) {
+    const float4* A = g_pool4 + PNT / 2;
+    const float4 x = A[i], y = A[n + i];
+    const float z = reinterpret_cast<const float*>(A + 2 * (size_t)n)[i];
+    a0 = x;
+    a1 = make_float4(x.w, y.x, y.y, 0.f);
+    a2 = make_float4(y.z, y.w, z, 0.f);
+}
+template <int PNT>
+__device__ __forceinline__ float4 pool_sphere(uint32_t i) { return (g_pool4 + PNT / 2)[i]; }
+// The whole workgroup copies the pool from prim4 (sc.n_pool primitives); a __syncthreads follows.
+template <int PNT>
+__device__ __forceinline__ void pool_fill(const DevScene& sc) {
+    float4* A = g_pool4 + PNT / 2;
+    float* C = reinterpret_cast<float*>(A + 2 * (size_t)sc.n_pool);
+    for (uint32_t i = threadIdx.x; i < sc.n_pool; i += PNT) {
+        const float4* p = sc.prim4 + 3 * (size_t)i;
+        const float4 p0 = p[0], p1 = p[1], p2 = p[2];
+        const bool sph = i < sc.pool_ftri;  // spheres lead the pool
+        A[i] = make_float4(p0.x, p0.y, p0.z, sph ? p0.w : p1.x);
+        A[sc.n_pool + i] = sph ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(p1.y, p1.z, p2.x, p2.y);
+        C[i] = sph ? 0.f : p2.z;
+    }
+}
+
 // Inclusive prefix maximum over the 64 lanes (the DPP pattern of wave_incl_scan with max).
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
@@ -793,13 +838,14 @@ constexpr uint32_t SLAB_NONE = 0x80000000u;  // a lane's slab delta when its lea
 // Returns the lane's leaf minimum as (bits(l) << 32 | index into sc.refs), ~0 for none; one
 // leaf's refs are contiguous, so the index orders like the position in the leaf.  `key0` is
 // the lane's minimum over refs it tested itself (the leaf's leading spheres).
-template <bool SLAB>
+template <bool SLAB, int PNT = 0>
 __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
                                                         uint32_t cnt, uint32_t lane, unsigned long long key0) {
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
-    __hip_atomic_store(&g_coop_key[threadIdx.x], key0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    unsigned long long* const keys = coop_keys<PNT>();
+    __hip_atomic_store(&keys[threadIdx.x], key0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     // slab index of item w of this lane's leaf = w + sdelta (SLAB_NONE: not staged); valid
     // deltas lie in (-2^31, RT_SLAB_TRIS), so the sentinel never collides
     uint32_t sdelta = SLAB_NONE;
@@ -866,23 +912,27 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
                 VC(2, 1);
-                VC(3, 3);
                 ref = sc.refs[idx];
-                const float4* pd = prim_data(sc, ref);
-                a0 = pd[0];
-                a1 = pd[1];
-                a2 = pd[2];
+                if constexpr (PNT > 0) {
+                    pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
+                } else {
+                    VC(3, 3);
+                    const float4* pd = prim_data(sc, ref);
+                    a0 = pd[0];
+                    a1 = pd[1];
+                    a2 = pd[2];
+                }
             }
             float l = 0.f, bu, bv;
             bool h;
             if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
             else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
             if (h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&g_coop_key[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
+                atomicMin(&keys[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
         }
     }
     if (SLAB) __builtin_amdgcn_wave_barrier();  // every read of this round's slab before the next fill
-    return __hip_atomic_load(&g_coop_key[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 // stack_search with cooperative leaves: the same per-lane traversal (kdtree.rs:66-104); lanes
@@ -897,7 +947,7 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
-template <bool FAST, bool RESTART, bool SLAB>
+template <bool FAST, bool RESTART, bool SLAB, int PNT = 0>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
                                                   uint32_t* st) {
@@ -996,7 +1046,9 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 for (uint32_t j = 0; j < lead; ++j) {
                     VC(4, 2);
                     float l;
-                    if (sphere_hit(prim_data(sc, sc.refs[off + j])[0], r, &l) && l >= HIT_MIN)
+                    const uint32_t sref = sc.refs[off + j];
+                    const float4 sph = PNT > 0 ? pool_sphere<PNT>(sref & REF_INDEX_MASK) : prim_data(sc, sref)[0];
+                    if (sphere_hit(sph, r, &l) && l >= HIT_MIN)
                         key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
                 }
                 off += lead;
@@ -1005,7 +1057,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         }
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
-        const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0)>(sc, r, off, cnt, lane, key0);
+        const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0), PNT>(sc, r, off, cnt, lane, key0);
         TM_ADD(12, TM_NOW() - tmc0);
         TM_ADD(13, (__shfl(wave_incl_scan(cnt, lane), 63) + 63u) / 64u);
         if (!done) {
@@ -1021,8 +1073,15 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             if (ret) {
                 VC(5, 4);
                 const uint32_t ref = sc.refs[(uint32_t)key];
-                const float4* pd = prim_data(sc, ref);
-                const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
+                float4 a0, a1, a2;
+                if constexpr (PNT > 0) {
+                    pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
+                } else {
+                    const float4* pd = prim_data(sc, ref);
+                    a0 = pd[0];
+                    a1 = pd[1];
+                    a2 = pd[2];
+                }
                 float l = 0.f, bu = 0.f, bv = 0.f;
                 if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(a0, r, &l);
                 else (void)tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
@@ -1183,7 +1242,7 @@ __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax,
 
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
-template <bool RESTART, bool SLAB>
+template <bool RESTART, bool SLAB, int PNT = 0>
 __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
                                              uint32_t* st, bool active, bool camera = false,
                                              const PkScene* ps = nullptr) {
@@ -1221,9 +1280,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     TM_ADD(8, __popcll(__ballot(in_coop)));
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
-            found = stack_search_coop<true, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<true, RESTART, SLAB, PNT>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
         else
-            found = stack_search_coop<false, RESTART, SLAB>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<false, RESTART, SLAB, PNT>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
     }
     TM_ADD(1, TM_NOW() - tm1);
     if (found) return true;
@@ -1595,7 +1654,8 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     return ++p.depth >= MAX_BOUNCES;
 }
 
-template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool SLAB = false>
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool SLAB = false,
+          int PNT = 0>
 __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true, const PkScene* ps = nullptr) {
     if (COUNT) c.segments++;
@@ -1604,7 +1664,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop<RESTART, SLAB>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
+    const bool hit = COOP ? closest_coop<RESTART, SLAB, PNT>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
                           : closest<COUNT, GEN, RESTART>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
@@ -1852,10 +1912,18 @@ __device__ __forceinline__ void make_start(const LaunchArgs& a, const DevScene& 
     e[5][lane] = slot;
 }
 
-template <bool GEN, bool DLS, bool RESTART, bool SLAB = false>
-__global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(LaunchArgs a, const uint2* __restrict__ pk_nodes,
-                                                                                const uint32_t* __restrict__ pk_refs,
-                                                                                const float4* __restrict__ pk_prim4) {
+// PNT > 0: the pool kernel (whole-pool residency, see g_pool4), PNT threads per workgroup; its
+// occupancy is one or two workgroups per CU (queue_lds_bytes), its traversal stackless.
+template <int PNT>
+constexpr int queue_min_waves(bool gen) {
+    return PNT == 768 ? 6 : (PNT == 1024 ? 4 : (gen ? RT_MIN_WAVES_GEN : RT_MIN_WAVES));
+}
+template <bool GEN, bool DLS, bool RESTART, bool SLAB = false, int PNT = 0>
+__global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) void queue_kernel(
+    LaunchArgs a, const uint2* __restrict__ pk_nodes, const uint32_t* __restrict__ pk_refs,
+    const float4* __restrict__ pk_prim4) {
+    static_assert(PNT == 0 || (GEN && RESTART && !SLAB && !DLS), "the pool kernel is the stackless general one");
+    constexpr uint32_t TPB = PNT > 0 ? (uint32_t)PNT : (uint32_t)BLOCK;  // threads per workgroup
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
     TM_VAR(const unsigned long long tm_start = TM_NOW());
@@ -1863,12 +1931,16 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         fill_lds_spheres(sc);
         __syncthreads();
     }
+    if constexpr (PNT > 0) {  // the whole pool, once per workgroup
+        pool_fill<PNT>(sc);
+        __syncthreads();
+    }
     uint32_t* st = GEN ? dyn_lds + threadIdx.x
                        : a.gstack + (size_t)blockIdx.x * BLOCK * sc.stack_depth + threadIdx.x;
     Ctr<false> c;
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
-    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    const uint32_t n_waves = gridDim.x * (TPB / 64);
     const bool batch_ok = !GEN && !sc.has_lens && a.pix_q != nullptr;
     const uint32_t shard_waves = (n_waves + a.n_shards - 1) / a.n_shards;
     // (the batch starts use one counter over all the items: the first grab is sized for that)
@@ -2013,7 +2085,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
-        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB>(sc, p, st, c, have, &ps) && have
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB, PNT>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             if (GEN) VC(13, 1);
@@ -2096,23 +2168,34 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
 // with a traversal stack (DevScene::restart: 0 stack, 1 stackless, 2 stackless with the triangle
 // slabs of coop_leaf).  The stack is in LDS for the general kernels and in global memory for the
 // sphere-only one (queue_gstack_bytes); the stackless kernels need neither.
+// The pool kernel (DevScene::pool_nt: 768 or 1024 threads per workgroup) takes precedence over
+// the others; it is only chosen for the general kernel without direct-light sampling.
 template <class F>
 static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
     const uint32_t rs = a.sc.restart;
     if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
     if (a.sc.spheres_only) return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
+    if (a.sc.pool_nt == 768) return f(queue_kernel<true, false, true, false, 768>, true);
+    if (a.sc.pool_nt == 1024) return f(queue_kernel<true, false, true, false, 1024>, true);
     if (rs == 2) return f(queue_kernel<true, false, true, true>, true);
     return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
 }
+static bool pool_kernel(const LaunchArgs& a) { return a.sc.pool_nt && !a.sc.dls && !a.sc.spheres_only; }
+size_t pool_lds_bytes(uint32_t pool_nt, uint32_t n_pool) {
+    return (size_t)pool_nt * sizeof(unsigned long long) + (size_t)n_pool * 36u;
+}
 static size_t queue_lds_bytes(const LaunchArgs& a, bool gen) {
+    if (pool_kernel(a)) return pool_lds_bytes(a.sc.pool_nt, a.sc.n_pool);
     return (gen && !a.sc.restart) ? stack_lds_bytes(a) : 0;
 }
+uint32_t queue_block_threads(const LaunchArgs& a) { return pool_kernel(a) ? a.sc.pool_nt : (uint32_t)BLOCK; }
 
 // Resident workgroups per CU of the queue kernel this scene launches (its registers and LDS
 // stack decide): the queue grid is exactly that many workgroups per CU.
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks) {
     return with_queue_kernel(a, [&](auto k, bool gen) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, BLOCK, queue_lds_bytes(a, gen));
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, (int)queue_block_threads(a),
+                                                            queue_lds_bytes(a, gen));
     });
 }
 
@@ -2123,8 +2206,8 @@ size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks) {
 
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s) {
     return with_queue_kernel(a, [&](auto k, bool gen) {
-        hipLaunchKernelGGL(k, dim3(n_blocks), dim3(BLOCK), queue_lds_bytes(a, gen), s, a, a.sc.nodes, a.sc.refs,
-                           a.sc.prim4);
+        hipLaunchKernelGGL(k, dim3(n_blocks), dim3(queue_block_threads(a)), queue_lds_bytes(a, gen), s, a, a.sc.nodes,
+                           a.sc.refs, a.sc.prim4);
         return hipGetLastError();
     });
 }

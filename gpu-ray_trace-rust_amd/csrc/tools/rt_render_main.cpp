@@ -7,9 +7,12 @@
 // <frames-dir>/<n>.png, n from 1 as in the GPU branch; --frames r/N renders frames i with
 // i % N == r (frames are independent: N processes on N GPUs need no collective).  The mp4
 // muxing of main.rs:54-97 (openh264) is not reproduced.
+// --gpus N (devices 0..N-1) or --devices a,b,...: one frame over several devices in this one
+// process (rt_render_to_target_devices: row stripes per device, one gather per batch), SURVEY.md
+// §8e behind the C ABI; a device may repeat (several contexts on one GPU).
 // Usage: rt_render <scheme.yml|scheme.json> [no_ui] [--assets DIR] [--out FILE] [--device N]
-//                  [--seed S] [--width W] [--height H] [--spp N] [--batch B]
-//                  [--frames-dir DIR] [--frames r/N] [--max-frames K]
+//                  [--gpus N | --devices a,b,...] [--seed S] [--width W] [--height H] [--spp N]
+//                  [--batch B] [--frames-dir DIR] [--frames r/N] [--max-frames K]
 // Assets are read from DIR/<dir>.npz (default: assets_pack next to the library's parent).
 #include <cstdio>
 #include <cstdlib>
@@ -41,7 +44,8 @@ void on_batch(void* user, uint32_t done) {
 int usage() {
     std::fprintf(stderr,
                  "usage: rt_render <scheme.yml|scheme.json> [no_ui] [--assets DIR] [--out FILE] [--device N]\n"
-                 "                 [--seed S] [--width W] [--height H] [--spp N] [--batch B]\n"
+                 "                 [--gpus N | --devices a,b,...] [--seed S] [--width W] [--height H]\n"
+                 "                 [--spp N] [--batch B]\n"
                  "                 [--frames-dir DIR] [--frames r/N] [--max-frames K]\n");
     return 2;
 }
@@ -61,6 +65,7 @@ int main(int argc, char** argv) {
     unsigned long long seed = 0x5EED0001ull;
     long width = -1, height = -1, spp = -1, batch = -1, max_frames = -1;
     std::string frames_dir = "anim_frames";
+    std::vector<int> devices;  // several: one frame over these devices (rt_render_to_target_devices)
     unsigned frank = 0, fworld = 1;
     for (int i = 2; i < argc; ++i) {
         const std::string a = argv[i];
@@ -75,6 +80,22 @@ int main(int argc, char** argv) {
         else if (a == "--assets") assets = val();
         else if (a == "--out") out = val();
         else if (a == "--device") device = std::atoi(val());
+        else if (a == "--gpus") {
+            const int n = std::atoi(val());
+            if (n < 1) return usage();
+            devices.clear();
+            for (int d = 0; d < n; ++d) devices.push_back(d);
+        }
+        else if (a == "--devices") {
+            devices.clear();
+            std::stringstream ds(val());
+            std::string tok;
+            while (std::getline(ds, tok, ',')) {
+                if (tok.empty()) return usage();
+                devices.push_back(std::atoi(tok.c_str()));
+            }
+            if (devices.empty()) return usage();
+        }
         else if (a == "--seed") seed = std::strtoull(val(), nullptr, 0);
         else if (a == "--width") width = std::atol(val());
         else if (a == "--height") height = std::atol(val());
@@ -104,6 +125,14 @@ int main(int argc, char** argv) {
     }
     rt_scheme_view v{};
     rt_scheme_view_get(sch, &v);
+    // one device: rt_render_to_target; several: the same loop over every device's stripes
+    auto render = [&](const rt_scheme_view& sv, uint8_t* target, uint32_t n_spp, uint32_t n_batch, Out* o) {
+        if (devices.size() > 1)
+            return rt_render_to_target_devices(sv.scene, sv.cam, sv.info, n_spp, n_batch, devices.data(),
+                                               (uint32_t)devices.size(), target, on_batch, o);
+        return rt_render_to_target(sv.scene, sv.cam, sv.info, n_spp, n_batch, devices.empty() ? device : devices[0],
+                                   target, on_batch, o);
+    };
     if (!v.use_gpu)
         std::fprintf(stderr, "rt_render: use_gpu is false in the scheme; rendering on the device path anyway\n");
     if (width > 0) v.info->width = (uint32_t)width;
@@ -136,7 +165,7 @@ int main(int argc, char** argv) {
             rt_scheme_view_get(fr, &fv);
             std::vector<uint8_t> target((size_t)fv.info->width * fv.info->height * 4, 0);
             Out o{frames_dir + "/" + std::to_string(i + 1) + ".png", target.data(), fv.info->width, fv.info->height, n_spp};
-            st = rt_render_to_target(fv.scene, fv.cam, fv.info, n_spp, n_batch, device, target.data(), on_batch, &o);
+            st = render(fv, target.data(), n_spp, n_batch, &o);
             rt_scheme_free(fr);
             std::fprintf(stderr, "\n");
             if (st != RT_OK || o.status != RT_OK) {
@@ -150,7 +179,7 @@ int main(int argc, char** argv) {
     }
     std::vector<uint8_t> target((size_t)v.info->width * v.info->height * 4, 0);
     Out o{out, target.data(), v.info->width, v.info->height, n_spp};
-    st = rt_render_to_target(v.scene, v.cam, v.info, n_spp, n_batch, device, target.data(), on_batch, &o);
+    st = render(v, target.data(), n_spp, n_batch, &o);
     std::fprintf(stderr, "\n");
     rt_scheme_free(sch);
     if (st != RT_OK) {

@@ -134,6 +134,7 @@ class FrameSteps:
 
     def step(self, gather: bool = True):
         torch = self.torch
+        self.host_frame_parts = None  # run()'s host copy is stale once another step runs
         if self.sync:
             self.ctx.render_device(self.out.data_ptr(), self.tiles, self.sample, self.spp_rank)
             self.sync_stats.append(self.ctx.launch_stats())  # each synchronous call is its own window

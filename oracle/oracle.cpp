@@ -79,7 +79,8 @@ static thread_local rt_rng_state g_rng;
 // MIX_NODE_D0 + d: branch nodes the traversal steps through at depth d (root = 0), the
 // counted renders' descent profile (how much of a descent a top-of-tree node cache could hold)
 enum { MIX_SPEC, MIX_DIFF, MIX_DIFFSPEC_DIFF, MIX_DIFFSPEC_SPEC, MIX_DIELECTRIC, MIX_RR, MIX_DRAWS, MIX_MESH,
-       MIX_POSDISC, MIX_NODE_D0, MIX_N = MIX_NODE_D0 + 40 };
+       MIX_POSDISC, MIX_NODE_D0, MIX_N = MIX_NODE_D0 + ORACLE_MIX_DEPTHS };
+static_assert(MIX_N == ORACLE_MIX_N, "oracle.h ORACLE_MIX_N");
 static thread_local uint64_t* g_mix = nullptr;
 #define MIX(i) do { if (g_mix) g_mix[i]++; } while (0)
 static std::mutex g_mix_mu;

@@ -54,8 +54,11 @@ int oracle_render_ex(const rt_scene_desc* scene, const rt_camera* cam, const rt_
 
 /* Shading mix of the counted renders (counts != NULL) since the last reset: continued rays by
  * material branch {spec, diff, diffspec->diff, diffspec->spec, dielectric}, Russian-roulette
- * draws, all draws, mesh continues. */
-void oracle_mix_counts(uint64_t out[9], int reset);
+ * draws, all draws, mesh continues, positive discriminants, then ORACLE_MIX_DEPTHS bins of branch
+ * nodes stepped through per depth: ORACLE_MIX_N entries in all. */
+#define ORACLE_MIX_DEPTHS 40
+#define ORACLE_MIX_N (9 + ORACLE_MIX_DEPTHS)
+void oracle_mix_counts(uint64_t out[ORACLE_MIX_N], int reset);
 
 /* KdTree::build (kdtree.rs:26-56,107-137) as a pointer tree, then a canonical depth-first
  * pre-order dump: per node {is_leaf, axis, split bits | leaf count, first ref}; refs in

@@ -436,7 +436,8 @@ def test_stackless_traversal_bit_invariant(gpu_available, oracle, monkeypatch, s
     """Stackless kd-restart with push-down (RT_DEBUG_KD_RESTART=1: after a leaf, descend again from the
     deepest node above the first push, entry = the leaf's exit) and the stackless kernel with the
     leaves' triangles staged in LDS (RT_DEBUG_KD_RESTART=2) each render the forward oracle's image (the
-    reference's stack traversal, kdtree.rs:66-104), bit for bit, in the queue kernels."""
+    reference's stack traversal, kdtree.rs:66-104), bit for bit, in the queue kernels; so does the
+    pool kernel (RT_DEBUG_POOL: the whole primitive pool resident in LDS)."""
     from rt_amd import render
 
     sc = load_scene(scene_name)
@@ -448,6 +449,15 @@ def test_stackless_traversal_bit_invariant(gpu_available, oracle, monkeypatch, s
         with render.Context(sc) as c:
             g = c.render(tiles, 0, spp)
         assert np.array_equal(g, o), (rs, parity.stats(g, o))
+    monkeypatch.delenv("RT_DEBUG_KD_RESTART")
+    # the pool kernel (every primitive resident in LDS, stackless), where the pool fits: 768 and
+    # 1024 threads per workgroup (triangles.yml, spaceship_r1; biplane / a380 do not fit: the
+    # request falls back to the general kernel and the image is the same)
+    for pool in ("768", "1024", "auto"):
+        monkeypatch.setenv("RT_DEBUG_POOL", pool)
+        with render.Context(sc) as c:
+            g = c.render(tiles, 0, spp)
+        assert np.array_equal(g, o), (pool, parity.stats(g, o))
 
 
 @pytest.mark.parametrize("scene_name,spp", [("triangles", 4), ("biplane", 3), ("spaceship_r1", 3), ("a380", 2)])

@@ -203,17 +203,19 @@ def test_rt_render_cli_usage():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["walled", "triangles"])
-def test_rt_render_cli_equals_python_host(gpu_available, tmp_path, name):
+@pytest.mark.parametrize("name,devs", [("walled", []), ("triangles", []), ("walled", ["--devices", "0,0,0"]),
+                                       ("biplane", ["--gpus", "1"])])
+def test_rt_render_cli_equals_python_host(gpu_available, tmp_path, name, devs):
     """C++ host end to end (scheme -> rt_render_to_target -> flipped PNG) == the Python host's
-    render_to_target on the same scheme, pixel for pixel."""
+    render_to_target on the same scheme, pixel for pixel; with --devices, one frame over several
+    contexts (rt_render_to_target_devices) gives the same PNG."""
     import subprocess
 
     from rt_amd import render, scheme
 
     out = str(tmp_path / "render_out.png")
     r = subprocess.run([RT_RENDER, os.path.join(SCENES, name + ".json"), "no_ui", "--assets", ASSETS, "--out", out,
-                        "--width", "96", "--height", "48", "--spp", "6", "--batch", "3"],
+                        "--width", "96", "--height", "48", "--spp", "6", "--batch", "3"] + devs,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     png = read_png_rgba(out)
