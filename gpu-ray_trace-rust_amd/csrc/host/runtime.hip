@@ -22,9 +22,6 @@
 #include "../../../include/rt_abi.h"
 #include "../../../include/rt_rng.h"
 #include "../kernel/device_scene.h"
-#ifndef RT_LDS_SPHERES
-#define RT_LDS_SPHERES 64  // must match trace.hip
-#endif
 #include "host_internal.h"
 #include "mesh_flatten.h"
 
@@ -164,9 +161,7 @@ static int guarded(rt_ctx* c, F f) {
     }
 }
 
-#ifndef RT_PIX_BLOCK
-#define RT_PIX_BLOCK 8  // queue order of a launch's pixels: B x B blocks of each tile (1: row order)
-#endif
+constexpr uint32_t RT_PIX_BLOCK = 8;  // queue order of a launch's pixels: B x B blocks of each tile (1: row order)
 
 // A/B and test knobs of the runtime, all named RT_DEBUG_<name> (INTEGRATION.md lists them), read
 // here; the host KD build reads its own two, RT_DEBUG_KD_THREADS and RT_DEBUG_KD_BUDGET
@@ -656,7 +651,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.n_spheres = scene->n_spheres;
     // the sphere-only kernel reads every sphere from its LDS table (trace.hip fetch_sphere)
     // (DLS runs in the general kernel)
-    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty() && scene->n_spheres <= RT_LDS_SPHERES && !d.dls) ? 1u : 0u;
+    d.spheres_only = (scene->n_free_tris == 0 && mf.tris.empty() && scene->n_spheres <= LDS_SPHERES && !d.dls) ? 1u : 0u;
     for (int i = 0; i < 6; ++i) d.bounds[i] = tree->bounds[i];
 
     // RayCompute::new (generate.rs:13-23)

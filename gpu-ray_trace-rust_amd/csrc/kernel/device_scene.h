@@ -7,10 +7,8 @@
 
 namespace rtd {
 
-#ifndef RT_BLOCK
-#define RT_BLOCK 128
-#endif
-constexpr int BLOCK = RT_BLOCK;  // threads per workgroup: 16 x (BLOCK/16) pixels at K = 1
+constexpr int BLOCK = 128;       // threads per workgroup: 16 x (BLOCK/16) pixels at K = 1
+constexpr int LDS_SPHERES = 64;  // the sphere-only kernel's LDS sphere tables (1 KiB each)
 constexpr int BLOCK_W = 16;
 constexpr int BLOCK_H = BLOCK / BLOCK_W;
 constexpr int MAX_STACK = 64;    // deepest KD tree the device path accepts (stack in LDS)

@@ -13,7 +13,11 @@
 //                  5 winner re-test, 6 path-start pixel table, 7 mesh shading records, 8 textures,
 //                  9 sphere / free-triangle shading, 10 packet leaf visits (scalar loads: no
 //                  VMEM), 11 cooperative passes, 12 cooperative rounds, 13 radiance stores
-//                  (writes), 14 path starts, 15-21 leaf sharing per round.
+//                  (writes), 14 path starts, 15-21 leaf sharing per round.  VL(class, address,
+//                  bytes) beside a load counts, per wave execution, the distinct 128-B lines, 64-B
+//                  sectors and lane addresses the load's active lanes touch (the requests that
+//                  load can send towards L2), and its lanes: which class pulls lines it does
+//                  not use (tools/vmem_classes.py).
 // Included by trace.hip after the kernel helpers it calls (wave_incl_scan).
 #pragma once
 
@@ -53,8 +57,38 @@ __device__ unsigned long long g_vc[24];
 __device__ unsigned int g_vc_waves;
 #define VC(i, n) do { if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) \
                            atomicAdd(&::rtd::g_vc[i], (unsigned long long)(n)); } while (0)
+// VL: per class, {active lanes, distinct 128-B lines, distinct 64-B sectors, bytes the distinct
+// lane addresses ask for (distinct addresses x the access's bytes)}
+__device__ unsigned long long g_vl[16][4];
+__device__ __forceinline__ uint32_t vl_distinct(uint64_t key, uint64_t mask) {
+    uint32_t n = 0;
+    while (mask) {
+        const uint32_t ld = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, (int)ld);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), (int)ld);
+        mask &= ~__ballot(key == (((uint64_t)hi << 32) | lo));
+        ++n;
+    }
+    return n;
+}
+__device__ __forceinline__ void vl_count(uint32_t cls, uint64_t addr, uint32_t nbytes, bool act) {
+    const uint64_t m = __ballot(act);
+    if (!m) return;
+    const uint32_t lanes = (uint32_t)__popcll(m);
+    const uint32_t lines = vl_distinct(act ? addr >> 7 : ~0ull, m);
+    const uint32_t secs = vl_distinct(act ? addr >> 6 : ~0ull, m);
+    const uint32_t addrs = vl_distinct(act ? addr : ~0ull, m);
+    if (__lane_id() == (uint32_t)__builtin_amdgcn_readfirstlane((int)__lane_id())) {
+        atomicAdd(&g_vl[cls][0], (unsigned long long)lanes);
+        atomicAdd(&g_vl[cls][1], (unsigned long long)lines);
+        atomicAdd(&g_vl[cls][2], (unsigned long long)secs);
+        atomicAdd(&g_vl[cls][3], (unsigned long long)addrs * nbytes);
+    }
+}
+#define VL(cls, ptr, nbytes, act) ::rtd::vl_count((cls), (uint64_t)(uintptr_t)(ptr), (nbytes), (act))
 #else
 #define VC(i, n) do { } while (0)
+#define VL(cls, ptr, nbytes, act) do { } while (0)
 #endif
 
 // RT_REGION_COUNT: wave-level executions of the sphere-only kernel's code regions (the first
@@ -142,7 +176,7 @@ __device__ __forceinline__ void diag_round_sharing(uint32_t off, uint32_t cnt) {
 template <bool GEN>
 __device__ __forceinline__ void diag_wave_exit() {
 #if RT_REGION_COUNT
-    if (__lane_id() == 0 && atomicAdd(&g_rc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+    if (__lane_id() == 0 && atomicAdd(&g_rc_waves, 1u) == gridDim.x * (blockDim.x / 64) - 1u) {
         __threadfence();
         for (int i = 0; i < RC_N; ++i) printf("RT_RC %d %llu\n", i, g_rc[i]);
         for (int i = 0; i < RC_N; ++i) g_rc[i] = 0;
@@ -150,15 +184,18 @@ __device__ __forceinline__ void diag_wave_exit() {
     }
 #endif
 #if RT_VMEM_COUNT
-    if (GEN && __lane_id() == 0 && atomicAdd(&g_vc_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+    if (GEN && __lane_id() == 0 && atomicAdd(&g_vc_waves, 1u) == gridDim.x * (blockDim.x / 64) - 1u) {
         __threadfence();
         for (int i = 0; i < 24; ++i) printf("RT_VC %d %llu\n", i, g_vc[i]);
         for (int i = 0; i < 24; ++i) g_vc[i] = 0;
+        for (int i = 0; i < 16; ++i)
+            printf("RT_VL %d %llu %llu %llu %llu\n", i, g_vl[i][0], g_vl[i][1], g_vl[i][2], g_vl[i][3]);
+        for (int i = 0; i < 16; ++i) g_vl[i][0] = g_vl[i][1] = g_vl[i][2] = g_vl[i][3] = 0;
         g_vc_waves = 0;
     }
 #endif
 #if RT_TIMING
-    if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (BLOCK / 64) - 1u) {
+    if (__lane_id() == 0 && atomicAdd(&g_tm_waves, 1u) == gridDim.x * (blockDim.x / 64) - 1u) {
         __threadfence();
         printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
                "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu | "

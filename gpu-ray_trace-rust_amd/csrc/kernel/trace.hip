@@ -34,50 +34,25 @@
 #include "device_scene.h"
 #include "diag.h"  // instrumentation of the diagnostic builds only (make diag); empty here
 
-#ifndef RT_REGEN_MIN
-#define RT_REGEN_MIN 12     // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
-#endif
-#ifndef RT_REGEN_MIN_BATCH
-#define RT_REGEN_MIN_BATCH 1 // the sphere-only kernel with batched starts (RT_START_BATCH): a start costs a few LDS reads, so idle lanes start at once (walled +6.5%; 4: +4.8%, 8: +3.5%); lens cameras, which keep per-lane starts, use it too
-#endif
-#ifndef RT_REGEN_MIN_GEN
-#define RT_REGEN_MIN_GEN 16 // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
-#endif
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 7      // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
-#endif
-#ifndef RT_MIN_WAVES_GEN
-#define RT_MIN_WAVES_GEN 8  // general (triangle / mesh) kernels: 8 -> <=64 VGPRs; latency-bound, +2..7% over 7 (spills outside the pass loop)
-#endif
-#ifndef RT_SLAB_TRIS
-#define RT_SLAB_TRIS 96     // stackless general kernel: primitives per wave staged in LDS per round (0: none)
-#endif
-#ifndef RT_OWNER_LOOP
-#define RT_OWNER_LOOP 8     // cooperative pass: owners of a pass found by a readlane loop when at most this many leaves end in it (0: binary search)
-#endif
-#ifndef RT_PAIR_FETCH
-#define RT_PAIR_FETCH 1     // cooperative descent: a node's two children loaded together, before its decision (a380 +3%, biplane +3%)
-#endif
-#ifndef RT_PIX_KEY
-#define RT_PIX_KEY 1        // queue kernels: the pixel's stream key from the queue-order table (one SplitMix64 round per path start, not two)
-#endif
-#ifndef RT_START_BATCH
-#define RT_START_BATCH 1    // sphere-only queue kernel: camera rays made 64 at a time, at full wave width, and handed out from LDS
-#endif
-#ifndef RT_PACKET
-#define RT_PACKET 1         // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
-#endif
-#ifndef RT_LEAF_REUSE
-#define RT_LEAF_REUSE 1     // cooperative search: a leaf whose ref list is the previous leaf's reuses its minimum
-#endif
-#ifndef RT_PACKET_MIN
-#define RT_PACKET_MIN 40    // fewest camera rays of one direction octant that form a packet
-#endif
-#ifndef RT_LDS_SPHERES
-#define RT_LDS_SPHERES 64   // 1 KiB
-#endif
+// Tuning constants (round 5: compile-time switches folded into constants; each value is the
+// measured best of its A/B).  LDS_SPHERES lives in device_scene.h (the host
+// shares it).
 
 namespace rtd {
+
+constexpr int RT_REGEN_MIN = 12;  // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
+constexpr int RT_REGEN_MIN_BATCH = 1;  // the sphere-only kernel with batched starts (RT_START_BATCH): a start costs a few LDS reads, so idle lanes start at once (walled +6.5%; 4: +4.8%, 8: +3.5%); lens cameras, which keep per-lane starts, use it too
+constexpr int RT_REGEN_MIN_GEN = 16;  // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
+constexpr int RT_MIN_WAVES = 7;  // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
+constexpr int RT_MIN_WAVES_GEN = 8;  // general (triangle / mesh) kernels: 8 -> <=64 VGPRs; latency-bound, +2..7% over 7 (spills outside the pass loop)
+constexpr int RT_SLAB_TRIS = 96;  // stackless general kernel: primitives per wave staged in LDS per round (0: none)
+constexpr int RT_OWNER_LOOP = 8;  // cooperative pass: owners of a pass found by a readlane loop when at most this many leaves end in it (0: binary search)
+constexpr int RT_PAIR_FETCH = 1;  // cooperative descent: a node's two children loaded together, before its decision (a380 +3%, biplane +3%)
+constexpr int RT_PIX_KEY = 1;  // queue kernels: the pixel's stream key from the queue-order table (one SplitMix64 round per path start, not two)
+constexpr int RT_START_BATCH = 1;  // sphere-only queue kernel: camera rays made 64 at a time, at full wave width, and handed out from LDS
+constexpr int RT_PACKET = 1;  // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
+constexpr int RT_LEAF_REUSE = 1;  // cooperative search: a leaf whose ref list is the previous leaf's reuses its minimum
+constexpr int RT_PACKET_MIN = 40;  // fewest camera rays of one direction octant that form a packet
 
 constexpr float EPS = 1e-4f;            // src/lib.rs:20
 constexpr float HIT_MIN = EPS * 20.0f;  // closest_hit.rs:16
@@ -222,9 +197,9 @@ struct Ctr {
 // {c, fl(r * r)} and its material (the host launches that kernel only when they all fit).
 // The LDS copies are file-scope __shared__ arrays referenced directly, so loads from them are
 // ds_read (a pointer that may be LDS or global would become a slower FLAT load).
-__shared__ float4 g_lds_sph[RT_LDS_SPHERES];
-__shared__ float4 g_lds_csq[RT_LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
-__shared__ DevMat g_lds_mat[RT_LDS_SPHERES];
+__shared__ float4 g_lds_sph[LDS_SPHERES];
+__shared__ float4 g_lds_csq[LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
+__shared__ DevMat g_lds_mat[LDS_SPHERES];
 __device__ __forceinline__ uint2 fetch_node(const DevScene& sc, uint32_t i) { return sc.nodes[i]; }
 // GEN == false (sphere-only kernel): spheres come from LDS.  The general kernel reads them from
 // global memory.
@@ -235,7 +210,7 @@ __device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, uint32_t i) {
 }
 
 __device__ __forceinline__ void fill_lds_spheres(const DevScene& sc) {
-    const uint32_t n = sc.n_spheres < (uint32_t)RT_LDS_SPHERES ? sc.n_spheres : (uint32_t)RT_LDS_SPHERES;
+    const uint32_t n = sc.n_spheres < (uint32_t)LDS_SPHERES ? sc.n_spheres : (uint32_t)LDS_SPHERES;
     for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
         const float4 v = sc.sph[i];
         g_lds_sph[i] = v;
@@ -912,12 +887,16 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 // the primitive's three float4 are loaded before the kind is known (a sphere's
                 // are {c, r} and padding): one round trip to L2 after the ref, not two
                 VC(2, 1);
+                VL(2, sc.refs + idx, 4, true);
                 ref = sc.refs[idx];
                 if constexpr (PNT > 0) {
                     pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
                 } else {
                     VC(3, 3);
                     const float4* pd = prim_data(sc, ref);
+                    VL(3, pd, 16, true);
+                    VL(3, pd + 1, 16, true);
+                    VL(3, pd + 2, 16, true);
                     a0 = pd[0];
                     a1 = pd[1];
                     a2 = pd[2];
@@ -971,6 +950,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         } else {
             --sp;
             VC(1, sp ? 2 : 1);
+            VL(1, sc.nodes + st[sp * BLOCK], 8, true);
             const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
             float d;
             (void)split_t<FAST>(pn, ax, r, &d);
@@ -992,6 +972,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         if (!done) {
             uint2 nd = fetch_node(sc, node);
             VC(0, 1);
+            VL(0, sc.nodes + node, 8, true);
             pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
                 VC(0, 1);
@@ -1000,6 +981,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 // decision's arithmetic
                 const uint32_t cpair = nd.y >> 2;
                 uint4 pair = make_uint4(0u, 0u, 0u, 0u);
+                VL(0, sc.nodes + cpair, 16, true);
                 if (RT_PAIR_FETCH) {
                     {
                         const uint2* pp = sc.nodes + cpair;
@@ -1047,6 +1029,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                     VC(4, 2);
                     float l;
                     const uint32_t sref = sc.refs[off + j];
+                    VL(4, prim_data(sc, sref), 16, true);
                     const float4 sph = PNT > 0 ? pool_sphere<PNT>(sref & REF_INDEX_MASK) : prim_data(sc, sref)[0];
                     if (sphere_hit(sph, r, &l) && l >= HIT_MIN)
                         key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
@@ -1073,6 +1056,8 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             if (ret) {
                 VC(5, 4);
                 const uint32_t ref = sc.refs[(uint32_t)key];
+                VL(5, sc.refs + (uint32_t)key, 4, true);
+                VL(5, prim_data(sc, ref), 48, true);
                 float4 a0, a1, a2;
                 if constexpr (PNT > 0) {
                     pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
@@ -1118,12 +1103,8 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
 // once fewer than RT_PACKET_KEEP lanes reach the packet's next leaf the packet stops: its lanes
 // still searching (`live`) continue in the cooperative search from interval [entry, root_exit],
 // where the reference's stack traversal visits the same remaining leaves (kd-restart argument).
-#ifndef RT_PACKET_KEEP
-#define RT_PACKET_KEEP 40
-#endif
-#ifndef RT_PACKET_SIDE
-#define RT_PACKET_SIDE 1    // 1: at a branch the packet follows the child more of its active lanes need (the others deferred)
-#endif
+constexpr int RT_PACKET_KEEP = 40;
+constexpr int RT_PACKET_SIDE = 1;  // 1: at a branch the packet follows the child more of its active lanes need (the others deferred)
 
 template <bool FAST>
 __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax, bool pk, float& entry,
@@ -1371,6 +1352,7 @@ __device__ __forceinline__ V3 get_pixel(const DevScene& sc, uint32_t off, uint32
     uint32_t y = __builtin_isnan(fy) ? 0u : (uint32_t)truncf(fy);
     const size_t i = (size_t)off + (size_t)y * w + x;
     VC(8, 1);
+    VL(8, sc.texels8 ? (const void*)(sc.texels8 + i) : (const void*)(sc.texels + 3 * i), (sc.texels8 ? 4u : 12u), true);
     if (sc.texels8) {  // 4 B per texel instead of 12: each channel k / 255.0f, correctly rounded
         const uint32_t t = sc.texels8[i];
         return mk(u8_over_255(t & 0xffu), u8_over_255((t >> 8) & 0xffu), u8_over_255((t >> 16) & 0xffu));
@@ -1379,6 +1361,7 @@ __device__ __forceinline__ V3 get_pixel(const DevScene& sc, uint32_t off, uint32
 }
 __device__ __forceinline__ V3 tex_pixel(const DevScene& sc, int32_t t, float u, float v) {
     VC(8, 1);
+    VL(8, sc.tex + t, 16, true);
     const DevTex tx = sc.tex[t];
     return get_pixel(sc, tx.off, tx.w, tx.h, u, v);
 }
@@ -1495,6 +1478,9 @@ __device__ __forceinline__ void tex_coord(const float2* uv, const DevMeshTri& t,
                                           float* v) {
     float b0 = 1.0f - b2 - b1;
     VC(7, 3);
+    VL(7, uv + t.v[0], 8, true);
+    VL(7, uv + t.v[1], 8, true);
+    VL(7, uv + t.v[2], 8, true);
     float2 c0 = uv[t.v[0]], c1 = uv[t.v[1]], c2 = uv[t.v[2]];
     float su = 0.0f, sv = 0.0f;
     su = su + c0.x * b0;
@@ -1519,7 +1505,12 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
                                           Ctr<COUNT>& c) {
     if (COUNT) c.mesh_hits++;
     VC(7, 6);  // the 64-B triangle record and the 32-B primitive record
+    VL(7, sc.mtri + idx, 16, true);
+    VL(7, reinterpret_cast<const char*>(sc.mtri + idx) + 16, 16, true);
+    VL(7, reinterpret_cast<const char*>(sc.mtri + idx) + 32, 16, true);
+    VL(7, reinterpret_cast<const char*>(sc.mtri + idx) + 48, 16, true);
     const DevMeshTri t = sc.mtri[idx];
+    VL(7, sc.prims + t.prim, 32, true);
     const DevPrim pr = sc.prims[t.prim];
     const float b1 = h.bu, b2 = h.bv;
     V3 n;  // NormFromMesh::get_norm (:136-157)
@@ -1530,6 +1521,9 @@ __device__ __forceinline__ bool mesh_segment(const DevScene& sc, const Hit& h, u
     } else {
         V3 cum = mk(0.f, 0.f, 0.f);
         VC(7, 3);
+        VL(7, sc.vnorm + t.v[0], 16, true);
+        VL(7, sc.vnorm + t.v[1], 16, true);
+        VL(7, sc.vnorm + t.v[2], 16, true);
         cum = cum + xyz(sc.vnorm[t.v[0]]);
         cum = cum + xyz(sc.vnorm[t.v[1]]);
         cum = cum + xyz(sc.vnorm[t.v[2]]);
@@ -1802,22 +1796,14 @@ __device__ __forceinline__ void launch_pixel(const LaunchArgs& a, uint32_t o, in
 // saturates it) and balance is fine-grained at the end of the launch.  Each item's radiance goes
 // to radiance[j][o]; fold_kernel then applies the running mean in sample order, so the image is
 // the direct schedule's, bit for bit.
-#ifndef RT_QDIV
-#define RT_QDIV 16
-#endif
-#ifndef RT_QMAX
-#define RT_QMAX 1024
-#endif
+constexpr int RT_QDIV = 16;
+constexpr int RT_QMAX = 1024;
 // Smallest grab.  The sphere-only kernel's items are cheap (~6 segments of a brute-force loop), so
 // 64-item grabs at the end of a launch put every wave on the one counter about every 7 us and
 // the atomics serialise: 256 ran walled +1.6% (A/B, bit-identical).  Mesh items cost 30x more
 // and need the fine end-of-launch balance: 128 ran biplane -10%.
-#ifndef RT_QMIN
-#define RT_QMIN 64
-#endif
-#ifndef RT_QMIN_SPH
-#define RT_QMIN_SPH 256
-#endif
+constexpr int RT_QMIN = 64;
+constexpr int RT_QMIN_SPH = 256;
 // A grab must cover every lane of a wave that asks at once (up to 64 items: queue_kernel claims
 // at most one grab per refill), and grabs stay multiples of 64.
 static_assert(RT_QMIN >= 64 && RT_QMIN % 64 == 0, "RT_QMIN: a multiple of 64, at least 64");
@@ -2039,6 +2025,7 @@ __global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) v
                     V3 dir;
                     if (GEN) { VC(6, 1); VC(14, 1); }
                     if (a.pix_q) {  // item j * n_pix + q: the q-th pixel in queue order
+                        if (GEN) VL(6, a.pix_q + o, 16, true);
                         const uint4 e = a.pix_q[o];
                         x = (int)(e.x & 0xffffu);
                         y = (int)(e.x >> 16);
@@ -2114,9 +2101,7 @@ __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
     // (exact reciprocal + Markstein quotients under their range guard).  The samples' loads are
     // issued FOLD_U at a time ahead of the sequential fold: with few launch pixels (a rank's
     // share at N = 8: 90K threads) one load in flight per thread left the fold latency-bound.
-#ifndef RT_FOLD_U
-#define RT_FOLD_U 8
-#endif
+constexpr int RT_FOLD_U = 8;
     constexpr uint32_t FOLD_U = RT_FOLD_U;
     uint32_t j = 0;
     for (; j + FOLD_U <= a.sample_count; j += FOLD_U) {

@@ -20,7 +20,7 @@ for v in "$@"; do
   mkdir -p $O/$name
   for k in 1 2 3; do
     eval "C=\$P$k"
-    ( IFS=','; for kv in $envs; do export "$kv"; done
+    ( IFS=',' read -ra KVS <<< "$envs"; for kv in "${KVS[@]}"; do export "$kv"; done
       timeout -s KILL 200 rocprofv3 --pmc $C --output-format csv -d $O/$name/p$k -o run -- \
         python3 bench.py $ARGS --sync --no-cpu --no-roofline --no-configs > $O/$name/p$k.log 2>&1 ) || exit $k
   done

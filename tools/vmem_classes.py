@@ -14,6 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade",
          "pk_leaves", "passes", "rounds", "rad_stores", "starts"]
 LOADS = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade"]
+# RT_VL classes (diag.h VL): lines / sectors / asked bytes of the load sites by class
+VL_NAMES = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex"]
 
 CHILD = r"""
 import os, sys
@@ -45,6 +47,8 @@ def main(specs):
             print(json.dumps({"scene": scene, "error": r.stderr[-2000:]}))
             continue
         last = {int(c): int(v) for _, c, v in vc[-24:]}
+        vl = [l.split() for l in r.stdout.splitlines() if l.startswith("RT_VL ")]
+        vl_last = {int(x[1]): [int(v) for v in x[2:6]] for x in vl[-16:]} if len(vl) >= 32 else {}
         d = {k: last[i] for i, k in enumerate(NAMES)}
         gn = ["pairs", "pairs_g2", "pairs_g3", "pairs_g4", "pairs_g8", "quads", "groups"]
         g = {k: last[15 + i] for i, k in enumerate(gn)}
@@ -61,6 +65,25 @@ def main(specs):
                                    "frac_ge8": round(g["pairs_g8"] / g["pairs"], 4),
                                    "quad_slots_per_pair": round(4 * g["quads"] / g["pairs"], 4),
                                    "pairs_per_group": round(g["pairs"] / g["groups"], 2)}
+        if vl_last:
+            # per class and sample: lanes served, distinct 128-B lines and 64-B sectors the wave
+            # loads touch (the requests a load can send past L1), the bytes the distinct lane
+            # addresses ask for, and lines x 128 B over those bytes (what a 128-B fetch of every
+            # touched line would over-fetch)
+            cls = {}
+            for i, k in enumerate(VL_NAMES):
+                lanes, lines, secs, asked = vl_last.get(i, [0, 0, 0, 0])
+                if not lanes:
+                    continue
+                cls[k] = {"lanes": round(lanes / samples, 3), "lines_128": round(lines / samples, 3),
+                          "sectors_64": round(secs / samples, 3), "asked_B": round(asked / samples, 1),
+                          "line_B_over_asked": round(128 * lines / asked, 3) if asked else None}
+            tl = sum(v["lines_128"] for v in cls.values())
+            ta = sum(v["asked_B"] for v in cls.values())
+            out["lines_by_class"] = cls
+            out["lines_total"] = {"lines_128_per_sample": round(tl, 2), "sectors_64_per_sample":
+                                  round(sum(v["sectors_64"] for v in cls.values()), 2),
+                                  "asked_B_per_sample": round(ta, 1), "line_B_per_sample": round(128 * tl, 1)}
         for p in sorted(os.listdir(os.path.join(ROOT, "profiles"))):
             if p.endswith("_counters.json"):
                 c = json.load(open(os.path.join(ROOT, "profiles", p)))
