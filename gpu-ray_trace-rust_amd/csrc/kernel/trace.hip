@@ -53,6 +53,9 @@ constexpr int RT_START_BATCH = 1;  // sphere-only queue kernel: camera rays made
 constexpr int RT_PACKET = 1;  // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
 constexpr int RT_LEAF_REUSE = 1;  // cooperative search: a leaf whose ref list is the previous leaf's reuses its minimum
 constexpr int RT_PACKET_MIN = 40;  // fewest camera rays of one direction octant that form a packet
+#ifndef RT_PASS_PREFETCH
+#define RT_PASS_PREFETCH 0
+#endif
 
 constexpr float EPS = 1e-4f;            // src/lib.rs:20
 constexpr float HIT_MIN = EPS * 20.0f;  // closest_hit.rs:16
@@ -865,6 +868,54 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     }
     // item w of a lane's leaf is sc.refs[w + delta]
     const uint32_t delta = off - (incl - cnt);
+    if constexpr (!SLAB && RT_PASS_PREFETCH) {
+        // The passes software-pipelined by one ref: pass k's primitive loads go out at its start
+        // (its ref arrived during pass k - 1), then pass k + 1's owner, index and ref load, then
+        // pass k's test, so the ref's trip to L2 overlaps the previous pass instead of
+        // preceding the primitive's.
+        uint32_t owner = total ? pass_owner(incl, total, 0, lane) : 0u;
+        uint32_t idx = lane + __shfl(delta, owner);
+        uint32_t ref = lane < total ? sc.refs[idx] : 0u;
+        for (uint32_t base = 0; base < total; base += 64) {
+            VC(11, 1);
+            const uint32_t w = base + lane;
+            float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
+            if (w < total) {
+                VC(2, 1);
+                if constexpr (PNT > 0) {
+                    pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
+                } else {
+                    VC(3, 3);
+                    const float4* pd = prim_data(sc, ref);
+                    a0 = pd[0];
+                    a1 = pd[1];
+                    a2 = pd[2];
+                }
+            }
+            const uint32_t nb = base + 64;
+            uint32_t owner_n = 0, idx_n = 0, ref_n = 0;
+            if (nb < total) {  // wave-uniform
+                owner_n = pass_owner(incl, total, nb, nb + lane);
+                idx_n = nb + lane + __shfl(delta, owner_n);
+                if (nb + lane < total) ref_n = sc.refs[idx_n];
+            }
+            Ray ro;
+            ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+            ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+            if (w < total) {
+                float l = 0.f, bu, bv;
+                bool h;
+                if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
+                else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
+                if (h && l >= HIT_MIN)  // valid and not NaN
+                    atomicMin(&keys[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
+            }
+            owner = owner_n;
+            idx = idx_n;
+            ref = ref_n;
+        }
+        return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
     for (uint32_t base = 0; base < total; base += 64) {
         VC(11, 1);
         const uint32_t w = base + lane;
