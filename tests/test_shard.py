@@ -191,3 +191,18 @@ def test_frame_steps_gathers_world2(tmp_path, mode, gathers):
     mp.spawn(_frame_steps_worker, args=(2, _free_port(), mode, res), nprocs=2, join=True)
     ok, n_gathers, calls = np.load(res)
     assert ok and n_gathers == gathers and calls == 6
+
+
+def test_frame_after_more_steps_is_not_stale():
+    """run() keeps a host copy of the frame; a step() after run() must drop it, so
+    frame() then reassembles the current buffer (one rank, no collective) instead of returning
+    the frame from before that step."""
+    from rt_amd import shard
+
+    w, h, spp = 16, 8, 2
+    tiles = [(0, 0, w, h)]
+    fs = shard.FrameSteps(_PatternCtx(w), tiles, w, h, 0, 1, 8, spp, None)
+    fs.run(2, 1)
+    assert (fs.frame()[..., 1] == 3 * spp).all()
+    fs.step()
+    assert (fs.frame()[..., 1] == 4 * spp).all()
