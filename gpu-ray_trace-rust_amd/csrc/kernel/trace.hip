@@ -868,37 +868,31 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     }
     // item w of a lane's leaf is sc.refs[w + delta]
     const uint32_t delta = off - (incl - cnt);
-    if constexpr (!SLAB && RT_PASS_PREFETCH) {
+    if constexpr (!SLAB && RT_PASS_PREFETCH == 1) {
         // The passes software-pipelined by one ref: pass k's primitive loads go out at its start
-        // (its ref arrived during pass k - 1), then pass k + 1's owner, index and ref load, then
-        // pass k's test, so the ref's trip to L2 overlaps the previous pass instead of
-        // preceding the primitive's.
+        // (its ref arrived during pass k - 1), then pass k + 1's ref load, then pass k's test, so
+        // the ref's trip to L2 overlaps the previous pass instead of preceding the primitive's.
+        // Every load is issued unconditionally (lanes past the pairs read entry 0 of the refs /
+        // primitive 0), so no branch makes the compiler wait for all loads before the test.
         uint32_t owner = total ? pass_owner(incl, total, 0, lane) : 0u;
         uint32_t idx = lane + __shfl(delta, owner);
-        uint32_t ref = lane < total ? sc.refs[idx] : 0u;
+        uint32_t ref = sc.refs[lane < total ? idx : 0u];
         for (uint32_t base = 0; base < total; base += 64) {
             VC(11, 1);
             const uint32_t w = base + lane;
-            float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
-            if (w < total) {
-                VC(2, 1);
-                if constexpr (PNT > 0) {
-                    pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
-                } else {
-                    VC(3, 3);
-                    const float4* pd = prim_data(sc, ref);
-                    a0 = pd[0];
-                    a1 = pd[1];
-                    a2 = pd[2];
-                }
+            float4 a0, a1, a2;
+            if constexpr (PNT > 0) {
+                pool_load<PNT>(sc.n_pool, (w < total ? ref : 0u) & REF_INDEX_MASK, a0, a1, a2);
+            } else {
+                const float4* pd = prim_data(sc, w < total ? ref : 0u);
+                a0 = pd[0];
+                a1 = pd[1];
+                a2 = pd[2];
             }
             const uint32_t nb = base + 64;
-            uint32_t owner_n = 0, idx_n = 0, ref_n = 0;
-            if (nb < total) {  // wave-uniform
-                owner_n = pass_owner(incl, total, nb, nb + lane);
-                idx_n = nb + lane + __shfl(delta, owner_n);
-                if (nb + lane < total) ref_n = sc.refs[idx_n];
-            }
+            const uint32_t owner_n = pass_owner(incl, total, nb < total ? nb : base, nb + lane);
+            const uint32_t idx_n = nb + lane + __shfl(delta, owner_n);
+            const uint32_t ref_n = sc.refs[nb + lane < total ? idx_n : 0u];
             Ray ro;
             ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
             ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
