@@ -281,7 +281,7 @@ def cpu_baseline(loaded, spp, threads=None, reps=3, rows_step=1):
     frame at `spp` samples per pixel, one thread per CPU the process may use
     (the reference's rayon par_iter_mut uses all of them, draw_scene.rs:73).  The KD build and
     scene setup are timed apart (an oracle call with 0 samples), as SURVEY.md §8d asks.
-    `reps` timed repetitions: the median is `value`, with the min / max beside it, and the
+    `reps` timed repetitions: the fastest is `value`, with the median / min beside it, and the
     process CPU time over each call (os.times: every thread of this process) gives the CPU the
     threads actually got — `effective_cores` = CPU-seconds / wall-seconds — and a per-core rate.
     rows_step > 1 renders every rows_step-th row only (one-row tiles over the whole frame: the
@@ -320,6 +320,7 @@ def cpu_baseline(loaded, spp, threads=None, reps=3, rows_step=1):
                      "effective_cores": cpu / wall})
     vals = sorted(r["Msamples_s"] for r in runs)
     med = statistics.median(vals)
+    spread = (vals[-1] - vals[0]) / med
     eff = statistics.median(r["effective_cores"] for r in runs)
     model = "unknown"
     try:
@@ -331,17 +332,25 @@ def cpu_baseline(loaded, spp, threads=None, reps=3, rows_step=1):
         pass
     cores = min(threads, quota) if quota else threads
     what = f"full {w}x{h} frame" if rows_step <= 1 else f"every {rows_step}th row of the {w}x{h} frame ({npix} pixels)"
-    return {"value": round(med, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "reps": reps, "min": round(vals[0], 4), "max": round(vals[-1], 4),
-            "spread": round((vals[-1] - vals[0]) / med, 4),
-            "effective_cores": round(eff, 2), "value_per_effective_core": round(med / eff, 4),
-            "runs": [{k: round(v, 3) for k, v in r.items()} for r in runs],
-            "threads": threads, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "cpu_model": model,
-            "kd_build_s": round(t_build, 3),
-            "sample": f"{what}, {spp} spp (BASELINE.md §2), one untimed warm-up call at that spp, then {reps} calls on "
-                      f"{threads} threads, median "
-                      f"(KD build timed apart, CPU quota {quota or 'none'}); oracle/oracle.cpp recursive radiance; "
-                      f"effective_cores = process CPU-seconds / wall-seconds of each call"}
+    # value = the fastest call: identical calls on the box's shared host run at up to 3x different
+    # rates at the same CPU-seconds, pinned or not (profiles/r5_cpu_probe_*.jsonl), so the least
+    # disturbed call is the CPU's rate; it is also the baseline most favourable to the CPU
+    res = {"value": round(vals[-1], 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+           "reps": reps, "median": round(med, 4), "min": round(vals[0], 4), "max": round(vals[-1], 4),
+           "spread": round(spread, 4),
+           "effective_cores": round(eff, 2), "value_per_effective_core": round(vals[-1] / eff, 4),
+           "runs": [{k: round(v, 3) for k, v in r.items()} for r in runs],
+           "threads": threads, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "cpu_model": model,
+           "kd_build_s": round(t_build, 3),
+           "sample": f"{what}, {spp} spp (BASELINE.md §2), one untimed warm-up call at that spp, then {reps} calls on "
+                     f"{threads} threads, fastest call "
+                     f"(KD build timed apart, CPU quota {quota or 'none'}); oracle/oracle.cpp recursive radiance; "
+                     f"effective_cores = process CPU-seconds / wall-seconds of each call"}
+    if spread > 0.10:
+        res["spread_note"] = ("identical calls (same pixels, samples and seeds) ran at different rates with the "
+                              "same CPU-seconds per call: the shared host's per-core speed varies between calls, "
+                              "pinned to idle cores or not (profiles/r5_cpu_probe_*.jsonl); value is the fastest")
+    return res
 
 
 def kernel_label(loaded):

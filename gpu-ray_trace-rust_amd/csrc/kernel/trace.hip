@@ -53,12 +53,6 @@ constexpr int RT_START_BATCH = 1;  // sphere-only queue kernel: camera rays made
 constexpr int RT_PACKET = 1;  // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
 constexpr int RT_LEAF_REUSE = 1;  // cooperative search: a leaf whose ref list is the previous leaf's reuses its minimum
 constexpr int RT_PACKET_MIN = 40;  // fewest camera rays of one direction octant that form a packet
-#ifndef RT_PASS_PREFETCH
-#define RT_PASS_PREFETCH 0
-#endif
-#ifndef RT_PASS_BRANCHLESS
-#define RT_PASS_BRANCHLESS 0
-#endif
 
 constexpr float EPS = 1e-4f;            // src/lib.rs:20
 constexpr float HIT_MIN = EPS * 20.0f;  // closest_hit.rs:16
@@ -281,32 +275,6 @@ __device__ __forceinline__ bool tri_hit(V3 v0, V3 e1, V3 e2, const Ray& r, float
     *bu = u;
     *bv = v;
     return true;
-}
-
-// tri_hit without its early returns: the same operations in the same order, every rejection
-// test folded into the result, so a cooperative pass (64 different triangles per wave) runs the
-// test straight through instead of through the divergent branches' exec-mask bookkeeping.  The
-// reciprocal's IEEE fallback (|det| >= 2^60 or NaN) stays behind a wave-uniform test.  Values
-// of a rejected lane are never used; an accepted lane's l, u, v are tri_hit's bit for bit.
-__device__ __forceinline__ bool tri_hit_bf(V3 v0, V3 e1, V3 e2, const Ray& r, float* l, float* bu,
-                                           float* bv) {
-    const V3 ray_x_e2 = cross(r.d, e2);
-    const float det = dot(e1, ray_x_e2);
-    const bool ok_det = !(fabsf(det) < EPS);
-    float inv_det = rcp_exact(det);
-    const bool slow = ok_det && !(fabsf(det) < 0x1p60f);
-    if (__builtin_expect(__ballot(slow) != 0, 0)) {
-        if (slow) inv_det = 1.0f / det;
-    }
-    const V3 rhs = r.o - v0;
-    const float u = inv_det * dot(rhs, ray_x_e2);
-    const V3 rhs_x_e1 = cross(rhs, e1);
-    const float v = inv_det * dot(r.d, rhs_x_e1);
-    const float t = inv_det * dot(e2, rhs_x_e1);
-    *l = t;
-    *bu = u;
-    *bv = v;
-    return ok_det && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || (u + v) > 1.0f) && !(t < EPS);
 }
 
 // closest_ray_hit over one leaf (closest_hit.rs:6-30): first strict RayLen minimum among
@@ -897,85 +865,6 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     }
     // item w of a lane's leaf is sc.refs[w + delta]
     const uint32_t delta = off - (incl - cnt);
-    if constexpr (!SLAB && RT_PASS_PREFETCH == 1) {
-        // The passes software-pipelined by one ref: pass k's primitive loads go out at its start
-        // (its ref arrived during pass k - 1), then pass k + 1's ref load, then pass k's test, so
-        // the ref's trip to L2 overlaps the previous pass instead of preceding the primitive's.
-        // Every load is issued unconditionally (lanes past the pairs read entry 0 of the refs /
-        // primitive 0), so no branch makes the compiler wait for all loads before the test.
-        uint32_t owner = total ? pass_owner(incl, total, 0, lane) : 0u;
-        uint32_t idx = lane + __shfl(delta, owner);
-        uint32_t ref = sc.refs[lane < total ? idx : 0u];
-        for (uint32_t base = 0; base < total; base += 64) {
-            VC(11, 1);
-            const uint32_t w = base + lane;
-            float4 a0, a1, a2;
-            if constexpr (PNT > 0) {
-                pool_load<PNT>(sc.n_pool, (w < total ? ref : 0u) & REF_INDEX_MASK, a0, a1, a2);
-            } else {
-                const float4* pd = prim_data(sc, w < total ? ref : 0u);
-                a0 = pd[0];
-                a1 = pd[1];
-                a2 = pd[2];
-            }
-            const uint32_t nb = base + 64;
-            const uint32_t owner_n = pass_owner(incl, total, nb < total ? nb : base, nb + lane);
-            const uint32_t idx_n = nb + lane + __shfl(delta, owner_n);
-            const uint32_t ref_n = sc.refs[nb + lane < total ? idx_n : 0u];
-            Ray ro;
-            ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
-            ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
-            if (w < total) {
-                float l = 0.f, bu, bv;
-                bool h;
-                if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
-                else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
-                if (h && l >= HIT_MIN)  // valid and not NaN
-                    atomicMin(&keys[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
-            }
-            owner = owner_n;
-            idx = idx_n;
-            ref = ref_n;
-        }
-        return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
-    if constexpr (!SLAB && RT_PASS_BRANCHLESS) {
-        // The pass with its loads unconditional (lanes past the pairs read entry 0) and the
-        // test branch-free (tri_hit_bf; spheres only where some lane of the wave has one):
-        // fewer exec-mask instructions per pair.
-        for (uint32_t base = 0; base < total; base += 64) {
-            VC(11, 1);
-            const uint32_t w = base + lane;
-            const uint32_t owner = pass_owner(incl, total, base, w);
-            const uint32_t idx = w + __shfl(delta, owner);
-            Ray ro;
-            ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
-            ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
-            const bool act = w < total;
-            const uint32_t ref = sc.refs[act ? idx : 0u];
-            float4 a0, a1, a2;
-            if constexpr (PNT > 0) {
-                pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
-            } else {
-                const float4* pd = prim_data(sc, ref);
-                a0 = pd[0];
-                a1 = pd[1];
-                a2 = pd[2];
-            }
-            float l = 0.f, bu, bv;
-            bool h = tri_hit_bf(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
-            const bool sph = (ref >> REF_KIND_SHIFT) == K_SPHERE;
-            if (__builtin_expect(__ballot(act && sph) != 0, 0)) {
-                float ls = 0.f;
-                const bool hs = sphere_hit(a0, ro, &ls);
-                h = sph ? hs : h;
-                l = sph ? ls : l;
-            }
-            if (act && h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&keys[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
-        }
-        return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    }
     for (uint32_t base = 0; base < total; base += 64) {
         VC(11, 1);
         const uint32_t w = base + lane;
