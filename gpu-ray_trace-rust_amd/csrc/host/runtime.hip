@@ -742,18 +742,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         else if (mode == "1024" && fits(1024, LDS_CU)) d.pool_nt = 1024;
         if (d.pool_nt) d.restart = 1;  // the pool kernel is stackless (its LDS holds no stack)
     }
-    // The resumable general kernel (trace.hip CoopState): RT_DEBUG_RESUME=N stops a wave's
-    // cooperative search once at most N lanes still search (they resume beside the next rays).
-    d.resume = 0;
-    if (const char* e = debug_env("RESUME")) {
-        const unsigned long v = std::strtoul(e, nullptr, 10);
-        if (!d.spheres_only && !d.dls && d.pool_nt == 0 && d.restart != 2 && v < 48) d.resume = (uint32_t)v;
-    }
-    d.resume_regen = 0;
-    if (const char* e = debug_env("RESUME_REGEN")) {
-        const unsigned long v = std::strtoul(e, nullptr, 10);
-        if (v >= 1 && v <= 64) d.resume_regen = (uint32_t)v;
-    }
     // Overlapped launches pay off while a launch's drain tail is a sizeable share of it: mesh
     // launches (8-10 ms tails) and small sphere-only ones — walled's ~0.4 ms tail on
     // one rank's 90 M-sample share at N = 8 (9 ms): +3% overlapped, while at 180 M it is neutral

@@ -79,11 +79,6 @@ struct DevScene {
     // launch; pool_nt = its threads per workgroup (768 / 1024), 0 = off; n_pool = primitives.
     uint32_t pool_nt;
     uint32_t n_pool;
-    // The resumable general kernel (trace.hip CoopState): a wave's cooperative search stops once
-    // no more than `resume` lanes are still searching, and they resume beside the next segment's
-    // rays; 0 = off (every search runs to its end).
-    uint32_t resume;
-    uint32_t resume_regen;  // the resumable kernel: idle lanes that start new paths together (0: RT_REGEN_MIN_GEN)
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

@@ -926,49 +926,19 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
-//
-// The search's per-lane state lives in a CoopState, so that a wave can stop its search between
-// two rounds and resume it later (the resumable kernel, DevScene::resume): with `stop_at` > 0
-// the rounds stop once no more than stop_at lanes are still searching (only in a call that
-// started with more than stop_at + RESUME_GAIN of them); those lanes return with `searching`
-// set and their state, and the next call continues their searches exactly where they stopped.
-// A lane's search is a function of its own state alone, so where it pauses changes nothing.
-// The LDS stack (RESTART = false) stays in the lane's own slots meanwhile.
-struct CoopState {
-    float entry, exit_t, top_t, root_exit;
-    uint32_t node, restart;
-    int sp;
+template <bool FAST, bool RESTART, bool SLAB, int PNT = 0>
+__device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
+                                                  bool active, float root_entry, float root_exit, Hit* best,
+                                                  uint32_t* st) {
+    float entry = root_entry, exit_t = root_exit, top_t = root_exit;
+    uint32_t node = 0, restart = 0;
+    int sp = 0;
+    bool done = !active, found = false, pushed = false;
+    const uint32_t lane = __lane_id();
     // RT_LEAF_REUSE: the previous leaf's list (its offset in sc.refs: the upload gives identical
     // lists one copy, so equal offsets mean equal lists) and its minimum key
-    uint32_t prev_list;
-    unsigned long long prev_key;
-};
-__device__ __forceinline__ void coop_state_init(CoopState& s, float root_entry, float root_exit) {
-    s.entry = root_entry;
-    s.exit_t = s.top_t = s.root_exit = root_exit;
-    s.node = s.restart = 0;
-    s.sp = 0;
-    s.prev_list = ~0u;
-    s.prev_key = ~0ull;
-}
-constexpr uint32_t RESUME_GAIN = 16;
-
-template <bool FAST, bool RESTART, bool SLAB, int PNT = 0>
-__device__ __forceinline__ bool stack_search_coop_s(const DevScene& sc, const Ray& r, const RayAx& ax,
-                                                    CoopState& s, bool& searching, Hit* best, uint32_t* st,
-                                                    uint32_t stop_at) {
-    float& entry = s.entry;
-    float& exit_t = s.exit_t;
-    float& top_t = s.top_t;
-    const float root_exit = s.root_exit;
-    uint32_t& node = s.node;
-    uint32_t& restart = s.restart;
-    int& sp = s.sp;
-    uint32_t& prev_list = s.prev_list;
-    unsigned long long& prev_key = s.prev_key;
-    bool done = !searching, found = false, pushed = false;
-    const uint32_t lane = __lane_id();
-    const bool may_stop = stop_at > 0 && (uint32_t)__popcll(__ballot(!done)) > stop_at + RESUME_GAIN;
+    uint32_t prev_list = ~0u;
+    unsigned long long prev_key = ~0ull;
     // After a leaf that does not return: the reference's pop (or the kd-restart); false when the
     // interval is exhausted (the reference's empty stack).
     auto advance = [&]() -> bool {
@@ -996,7 +966,6 @@ __device__ __forceinline__ bool stack_search_coop_s(const DevScene& sc, const Ra
         return true;
     };
     while (__ballot(!done) != 0) {
-        if (may_stop && (uint32_t)__popcll(__ballot(!done)) <= stop_at) break;  // the rest resume later
         uint32_t off = 0, cnt = 0, list = ~0u;
         unsigned long long key0 = ~0ull;
         VC(12, 1);
@@ -1112,17 +1081,7 @@ __device__ __forceinline__ bool stack_search_coop_s(const DevScene& sc, const Ra
             }
         }
     }
-    searching = !done;
     return found;
-}
-template <bool FAST, bool RESTART, bool SLAB, int PNT = 0>
-__device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
-                                                  bool active, float root_entry, float root_exit, Hit* best,
-                                                  uint32_t* st) {
-    CoopState s;
-    coop_state_init(s, root_entry, root_exit);
-    bool searching = active;
-    return stack_search_coop_s<FAST, RESTART, SLAB, PNT>(sc, r, ax, s, searching, best, st, 0u);
 }
 
 // ------------------------------------------------------------ packet traversal (camera rays)
@@ -1314,66 +1273,6 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
         return true;
     }
     return false;
-}
-
-// closest_coop for the resumable kernel (DevScene::resume).  Lanes `fresh` start their segment's
-// search (camera rays through the packet first, as in closest_coop); lanes `tracing` continue the
-// search they stopped in an earlier call (state in cs).  Returns true for the lanes whose search
-// ended in this call, with the hit in *best and *hit (the cube map when nothing else); `tracing`
-// is left set for the lanes that stopped again.  Called by every lane of the wave.
-template <bool RESTART, int PNT>
-__device__ __forceinline__ bool closest_coop_resume(const DevScene& sc, const Ray& r, Hit* best, bool* hit,
-                                                    uint32_t* st, bool fresh, bool camera, bool& tracing,
-                                                    CoopState& cs, const PkScene* ps) {
-    float root_entry = 0.f, root_exit = 0.f;
-    const RayAx ax = ray_axes(r);
-    const bool in = fresh && sc.n_nodes && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit);
-    bool found = false;
-    const bool fast = !(in || tracing) || (sc.fastdiv && origin_fast_ok(r.o));
-    const bool all_fast = __ballot(!fast) == 0;
-    bool pk = false, pk_live = false;
-    TM_VAR(const unsigned long long tm0 = TM_NOW());
-    if (RT_PACKET && ps && sc.packet) {
-        const uint32_t oct = (ax.dx > 0.0f ? 1u : 0u) | (ax.dy > 0.0f ? 2u : 0u) | (ax.dz > 0.0f ? 4u : 0u);
-        const bool num = !__builtin_isnan(ax.dx) && !__builtin_isnan(ax.dy) && !__builtin_isnan(ax.dz);
-        const bool cand = in && camera && num;
-        const uint64_t cm = __ballot(cand);
-        if (__popcll(cm) >= RT_PACKET_MIN) {
-            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)cm) - 1u;
-            pk = cand && oct == (uint32_t)__builtin_amdgcn_readlane((int)oct, (int)lead);
-            if (__popcll(__ballot(pk)) >= RT_PACKET_MIN) {
-                found = all_fast ? closest_packet<true>(*ps, r, ax, pk, root_entry, root_exit, best, pk_live)
-                                 : closest_packet<false>(*ps, r, ax, pk, root_entry, root_exit, best, pk_live);
-            } else {
-                pk = false;
-            }
-        }
-    }
-    const bool start = in && (!pk || pk_live);
-    if (start) coop_state_init(cs, root_entry, root_exit);
-    TM_VAR(const unsigned long long tm1 = TM_NOW());
-    TM_ADD(0, tm1 - tm0);
-    TM_ADD(6, __popcll(__ballot(pk)));
-    TM_ADD(7, __popcll(__ballot(pk && pk_live)));
-    TM_ADD(8, __popcll(__ballot(start)));
-    bool searching = tracing || start;
-    const bool was = fresh || tracing;
-    if (__ballot(searching)) {
-        if (__builtin_expect(all_fast, 1))
-            found = stack_search_coop_s<true, RESTART, false, PNT>(sc, r, ax, cs, searching, best, st, sc.resume) || found;
-        else
-            found = stack_search_coop_s<false, RESTART, false, PNT>(sc, r, ax, cs, searching, best, st, sc.resume) || found;
-    }
-    TM_ADD(1, TM_NOW() - tm1);
-    tracing = searching;
-    const bool ended = was && !searching;
-    if (ended && !found && sc.has_cube) {
-        best->ref = REF_CUBE;
-        best->l = __builtin_inff();
-        found = true;
-    }
-    *hit = found;
-    return ended;
 }
 
 // ---------------------------------------------------------------- materials (interaction.rs)
@@ -1765,21 +1664,6 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
 }
 
-// segment() for the resumable kernel: a lane with a path either starts its next segment (its
-// ray normalized once, as segment() does) or continues the search it stopped; returns true when
-// the lane's path has ended in this call.
-template <bool RESTART, int PNT>
-__device__ __forceinline__ bool segment_resume(const DevScene& sc, Path& p, uint32_t* st, Ctr<false>& c,
-                                               bool have, bool& tracing, CoopState& cs, const PkScene* ps) {
-    const bool fresh = have && !tracing;
-    if (fresh) p.ray.d = normalize(p.ray.d);
-    Hit h;
-    bool hit = false;
-    const bool ended = closest_coop_resume<RESTART, PNT>(sc, p.ray, &h, &hit, st, fresh, p.depth == 0, tracing, cs, ps);
-    if (!(have && ended)) return false;
-    return shade<false, true, false>(sc, p, h, hit, c);
-}
-
 // key: the pixel's stream key, rt_rng_pixel_key(sc.seed, pixel) (rt_rng_init's first round)
 __device__ __forceinline__ void start_path(const DevScene& sc, Path& p, V3 dir, uint64_t key, uint64_t s) {
     p.rng = rt_rng_init_key(key, s);
@@ -2020,12 +1904,11 @@ template <int PNT>
 constexpr int queue_min_waves(bool gen) {
     return PNT == 768 ? 6 : (PNT == 1024 ? 4 : (gen ? RT_MIN_WAVES_GEN : RT_MIN_WAVES));
 }
-template <bool GEN, bool DLS, bool RESTART, bool SLAB = false, int PNT = 0, bool RESUME = false>
+template <bool GEN, bool DLS, bool RESTART, bool SLAB = false, int PNT = 0>
 __global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) void queue_kernel(
     LaunchArgs a, const uint2* __restrict__ pk_nodes, const uint32_t* __restrict__ pk_refs,
     const float4* __restrict__ pk_prim4) {
     static_assert(PNT == 0 || (GEN && RESTART && !SLAB && !DLS), "the pool kernel is the stackless general one");
-    static_assert(!RESUME || (GEN && !DLS && !SLAB), "the resumable kernel is the general one without DLS or slabs");
     constexpr uint32_t TPB = PNT > 0 ? (uint32_t)PNT : (uint32_t)BLOCK;  // threads per workgroup
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
@@ -2053,16 +1936,13 @@ __global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) v
     bool have = false, done = false;
     uint32_t slot = 0;                // radiance index of the lane's item
     Path p;
-    bool tracing = false;             // RESUME: the lane's segment search is stopped, its state in cs
-    CoopState cs;
     // RT_START_BATCH: the wave's current batch of starts, entries [st_pos, 64) not yet taken
     uint32_t st_pos = 64u, st_n = 0u;
     for (;;) {
         const uint64_t need = __ballot(!have && !done);
         // Starting paths is wave-wide work at the width of the idle lanes: ~10 of 64 lanes end a
         // path per segment, so without batched starts the wave waits for RT_REGEN_MIN of them.
-        const int regen_min = RESUME && sc.resume_regen ? (int)sc.resume_regen
-                                                        : (GEN ? RT_REGEN_MIN_GEN : (RT_START_BATCH ? RT_REGEN_MIN_BATCH : RT_REGEN_MIN));
+        constexpr int regen_min = GEN ? RT_REGEN_MIN_GEN : (RT_START_BATCH ? RT_REGEN_MIN_BATCH : RT_REGEN_MIN);
         const bool regen = need && (regen_min <= 1 || __popcll(need) >= regen_min || __ballot(have) == 0);
         if (!GEN && RT_START_BATCH && regen && batch_ok) {
             RC(RC_REGEN);
@@ -2192,10 +2072,8 @@ __global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) v
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
-        bool fin;
-        if constexpr (RESUME) fin = segment_resume<RESTART, PNT>(sc, p, st, c, have, tracing, cs, &ps);
-        else fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB, PNT>(sc, p, st, c, have, &ps) && have
-                       : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB, PNT>(sc, p, st, c, have, &ps) && have
+                             : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             if (GEN) VC(13, 1);
             if (!GEN) RC(RC_STORE);
@@ -2285,9 +2163,6 @@ static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
     if (a.sc.pool_nt == 768) return f(queue_kernel<true, false, true, false, 768>, true);
     if (a.sc.pool_nt == 1024) return f(queue_kernel<true, false, true, false, 1024>, true);
     if (rs == 2) return f(queue_kernel<true, false, true, true>, true);
-    if (a.sc.resume)
-        return rs ? f(queue_kernel<true, false, true, false, 0, true>, true)
-                  : f(queue_kernel<true, false, false, false, 0, true>, true);
     return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
 }
 static bool pool_kernel(const LaunchArgs& a) { return a.sc.pool_nt && !a.sc.dls && !a.sc.spheres_only; }
