@@ -12,7 +12,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <limits>
 #include <new>
 #include <string>
 #include <string_view>
@@ -173,156 +172,6 @@ static const char* debug_env(const char* name) {
     char key[64];
     std::snprintf(key, sizeof key, "RT_DEBUG_%s", name);
     return std::getenv(key);
-}
-
-// Shared-ref masks (trace.hip shared_mask): for two leaf lists that a ray can visit one after
-// the other, L after P, bit j of mask(L, P) says that ref j of L (j < 32) is also in P.  A ray
-// tested those refs in P, against the same ray, so its cooperative search tests only the others
-// in L and decides L's first minimum from them and P's minimum (trace.hip coop_leaf), or tests
-// the rest too when it cannot.  The pairs are the leaves that share a face: the ray leaves P
-// through the split plane it enters L by, so P's cell touches L's face on that plane (a face with
-// more than 64 such neighbours gets no masks; a pair without a mask is just tested in full).  The
-// table is open-addressed on (L, P) list offsets, each key within SHARED_PROBES slots of its
-// hash, {L, P, mask, 0} per slot, L = ~0 empty; masks of fewer than SHARED_MIN refs are left out,
-// and the leaves whose list has a mask carry LEAF_SHARED.
-static void build_shared_masks(std::vector<uint2>& nodes, const std::vector<uint32_t>& refs,
-                               std::vector<uint4>* tab) {
-    tab->clear();
-    if (nodes.empty()) return;
-    struct Leaf { float lo[3], hi[3]; uint32_t off, cnt; };
-    struct Cell { uint32_t node; float lo[3], hi[3]; };
-    std::vector<Leaf> leaves;
-    const float INF = std::numeric_limits<float>::infinity();
-    std::vector<Cell> stk;
-    stk.push_back(Cell{0, {-INF, -INF, -INF}, {INF, INF, INF}});
-    while (!stk.empty()) {
-        const Cell c = stk.back();
-        stk.pop_back();
-        const uint2 n = nodes[c.node];
-        if ((n.y & 3u) == RT_KD_LEAF) {
-            const uint32_t cnt = n.x & LEAF_COUNT_MASK;
-            if (cnt) leaves.push_back(Leaf{{c.lo[0], c.lo[1], c.lo[2]}, {c.hi[0], c.hi[1], c.hi[2]}, n.y >> 2, cnt});
-            continue;
-        }
-        const uint32_t a = n.y & 3u, ch = n.y >> 2;
-        float s;
-        std::memcpy(&s, &n.x, 4);
-        Cell lo = c, hi = c;
-        lo.node = ch;
-        lo.hi[a] = std::min(c.hi[a], s);
-        hi.node = ch + 1;
-        hi.lo[a] = std::max(c.lo[a], s);
-        stk.push_back(lo);
-        stk.push_back(hi);
-    }
-    // (L, P) pairs over every leaf's six faces, the leaves split over threads; a face whose
-    // neighbour search visits more than SHARED_VISITS nodes (degenerate, flat cells) gets none
-    constexpr size_t SHARED_VISITS = 512;
-    const unsigned n_thr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::vector<uint64_t>> part(n_thr);
-    auto work = [&](unsigned t) {
-    std::vector<uint64_t>& pairs = part[t];
-    std::vector<uint32_t> found;
-    std::vector<Cell> stk;
-    for (size_t li = t; li < leaves.size(); li += n_thr) {
-        const Leaf& L = leaves[li];
-        for (uint32_t a = 0; a < 3; ++a) {
-            for (int side = 0; side < 2; ++side) {
-                const float x = side ? L.hi[a] : L.lo[a];
-                if (!std::isfinite(x)) continue;
-                float qlo[3] = {L.lo[0], L.lo[1], L.lo[2]}, qhi[3] = {L.hi[0], L.hi[1], L.hi[2]};
-                qlo[a] = qhi[a] = x;
-                found.clear();
-                bool over = false;
-                size_t visits = 0;
-                stk.clear();
-                stk.push_back(Cell{0, {-INF, -INF, -INF}, {INF, INF, INF}});
-                while (!stk.empty() && !over) {
-                    const Cell c = stk.back();
-                    stk.pop_back();
-                    if (++visits > SHARED_VISITS) {
-                        over = true;
-                        break;
-                    }
-                    bool meets = true;
-                    for (int k = 0; k < 3; ++k) meets = meets && c.lo[k] <= qhi[k] && qlo[k] <= c.hi[k];
-                    if (!meets) continue;
-                    const uint2 n = nodes[c.node];
-                    if ((n.y & 3u) == RT_KD_LEAF) {
-                        const uint32_t cnt = n.x & LEAF_COUNT_MASK, off = n.y >> 2;
-                        // P on the other side of L's face: its cell ends (starts) on the plane
-                        if (cnt && off != L.off && (side ? c.lo[a] == x : c.hi[a] == x)) {
-                            if (found.size() == 64) over = true;
-                            else found.push_back(off);
-                        }
-                        continue;
-                    }
-                    const uint32_t ax = n.y & 3u, ch = n.y >> 2;
-                    float s;
-                    std::memcpy(&s, &n.x, 4);
-                    Cell lo = c, hi = c;
-                    lo.node = ch;
-                    lo.hi[ax] = std::min(c.hi[ax], s);
-                    hi.node = ch + 1;
-                    hi.lo[ax] = std::max(c.lo[ax], s);
-                    stk.push_back(lo);
-                    stk.push_back(hi);
-                }
-                if (over) continue;
-                for (uint32_t p : found) pairs.push_back(((uint64_t)L.off << 32) | p);
-            }
-        }
-    }
-    };
-    {
-        std::vector<std::thread> th;
-        for (unsigned t = 1; t < n_thr; ++t) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-    }
-    std::vector<uint64_t> pairs;
-    for (auto& v : part) pairs.insert(pairs.end(), v.begin(), v.end());
-    std::sort(pairs.begin(), pairs.end());
-    pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
-    if (pairs.empty()) return;
-    // list lengths by offset (every leaf's list, deduplicated lists share an offset)
-    std::unordered_map<uint32_t, uint32_t> len;
-    for (const Leaf& L : leaves) len[L.off] = L.cnt;
-    size_t cap = 16;
-    while (cap < 2 * pairs.size()) cap <<= 1;
-    tab->assign(cap, make_uint4(~0u, ~0u, 0u, 0u));
-    std::vector<uint32_t> ps, flagged;
-    uint32_t cur_p = ~0u;
-    // pairs sorted by L then P; P's list sorted once per run of equal P is not possible here, so
-    // each pair sorts P's (short) list
-    for (uint64_t k : pairs) {
-        const uint32_t l = (uint32_t)(k >> 32), p = (uint32_t)k;
-        const uint32_t nl = len[l], np = len[p];
-        if (p != cur_p) {
-            ps.assign(refs.begin() + p, refs.begin() + p + np);
-            std::sort(ps.begin(), ps.end());
-            cur_p = p;
-        }
-        uint32_t m = 0;
-        for (uint32_t j = 0; j < nl && j < 32; ++j)
-            if (std::binary_search(ps.begin(), ps.end(), refs[l + j])) m |= 1u << j;
-        if ((uint32_t)__builtin_popcount(m) < SHARED_MIN) continue;
-        const uint32_t h = shared_hash(l, p);
-        for (uint32_t q = 0; q < SHARED_PROBES; ++q) {
-            uint4& e = (*tab)[(h + q) & (cap - 1)];
-            if (e.x == ~0u) {
-                e = make_uint4(l, p, m, 0u);
-                flagged.push_back(l);
-                break;
-            }
-        }
-    }
-    // the leaves whose list has a mask look it up; the others never do
-    std::sort(flagged.begin(), flagged.end());
-    for (uint2& n : nodes)
-        if ((n.y & 3u) == RT_KD_LEAF && (n.x & LEAF_COUNT_MASK) &&
-            std::binary_search(flagged.begin(), flagged.end(), n.y >> 2))
-            n.x |= LEAF_SHARED;
 }
 
 template <class T>
@@ -604,7 +453,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     // tests them per lane and leaves only triangles to the wave's cooperative passes.
     for (uint2& n : nodes) {
         if ((n.y & 3u) != RT_KD_LEAF) continue;
-        if (n.x > LEAF_COUNT_MASK) return set_err(c, RT_ERR_UNSUPPORTED, "KD leaf with 2^23 refs or more");
+        if (n.x > LEAF_COUNT_MASK) return set_err(c, RT_ERR_UNSUPPORTED, "KD leaf with over 2^24 refs");
         const uint32_t off = n.y >> 2;
         uint32_t lead = 0;
         while (lead < n.x && lead < 255u && (refs[off + lead] >> REF_KIND_SHIFT) == K_SPHERE) ++lead;
@@ -645,18 +494,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         ftri_mat[i] = make_mat(t.mat, t.rgb);
     }
 
-    // shared-ref masks of the cooperative search (build_shared_masks); RT_DEBUG_SHARED=0: none
-    std::vector<uint4> pair_tab;
-    {
-        const char* e = debug_env("SHARED");
-        if ((!e || std::strcmp(e, "0")) && scene->n_free_tris + scene->n_meshes > 0)
-            build_shared_masks(nodes, refs, &pair_tab);
-        if (debug_env("CREATE_TIMING")) {
-            size_t used = 0;
-            for (const uint4& e : pair_tab) used += e.x != ~0u;
-            std::fprintf(stderr, "rt_create: shared-ref masks %zu in %zu slots\n", used, pair_tab.size());
-        }
-    }
     pc.mark("refs_dedupe_spheres");
     MeshFlat mf;
     if ((st = flatten_meshes(scene, &mf))) return set_err(c, st, "invalid mesh description");
@@ -721,10 +558,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.n_emit = (uint32_t)emit.size();
     d.dls = emit.empty() ? 0u : 1u;  // no emitter: the DLS term is exactly zero
     if ((st = upload(c, refs, &d.refs))) return st;
-    if (!pair_tab.empty()) {
-        if ((st = upload(c, pair_tab, &d.pair_tab))) return st;
-        d.pair_cap = (uint32_t)pair_tab.size() - 1u;
-    }
     if ((st = upload(c, sph, &d.sph))) return st;
     if ((st = upload(c, sph_mat, &d.sph_mat))) return st;
     {   // the leaf-test pool: spheres, free triangles, mesh triangles, 3 float4 each

@@ -16,17 +16,8 @@ constexpr int MAX_STACK = 64;    // deepest KD tree the device path accepts (sta
 // Leaf node (rt_kd_node {count, (offset << 2) | 3}) on the device: the low 24 bits of the first
 // word hold the ref count, the top 8 the number of sphere refs that open the leaf's list (refs
 // keep renderable order, where spheres usually precede every triangle; 0 when it does not fit).
-constexpr uint32_t LEAF_COUNT_MASK = (1u << 23) - 1u;
-constexpr uint32_t LEAF_SHARED = 1u << 23;  // the leaf's list has shared-ref masks (trace.hip shared_mask)
+constexpr uint32_t LEAF_COUNT_MASK = (1u << 24) - 1u;
 constexpr uint32_t LEAF_LEAD_SHIFT = 24;
-constexpr uint32_t SHARED_PROBES = 4;  // a shared-mask key lies within this many slots of its hash
-constexpr uint32_t SHARED_MIN = 4;     // fewest shared refs worth a mask
-__host__ __device__ inline uint32_t shared_hash(uint32_t l, uint32_t p) {  // slot of the shared-mask key (l, p)
-    uint32_t h = l * 0x9e3779b1u ^ (p + 0x7f4a7c15u) * 0x85ebca77u;
-    h ^= h >> 15;
-    h *= 0x2c1b3c6du;
-    return h ^ (h >> 12);
-}
 
 // Device ref encoding: kind in the top 2 bits, index into the kind's arrays below.
 constexpr uint32_t REF_KIND_SHIFT = 30;
@@ -88,10 +79,6 @@ struct DevScene {
     // launch; pool_nt = its threads per workgroup (768 / 1024), 0 = off; n_pool = primitives.
     uint32_t pool_nt;
     uint32_t n_pool;
-    // Shared-ref masks (runtime.hip build_shared_masks, trace.hip shared_mask): open-addressed
-    // {L list offset, P list offset, mask low, mask high}; pair_cap = slots - 1, 0 without a table.
-    const uint4* pair_tab;
-    uint32_t pair_cap;
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

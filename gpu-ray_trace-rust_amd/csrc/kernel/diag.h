@@ -199,9 +199,9 @@ __device__ __forceinline__ void diag_wave_exit() {
         __threadfence();
         printf("RT_TIMING packet %llu coop %llu wave %llu | pk_leaves %llu pk_lanes %llu pk_refs %llu | "
                "pk_rays %llu handed %llu coop_rays %llu | coop_rounds %llu coop_lanes %llu first_group %llu | "
-               "passes_time %llu passes %llu | shared_skipped %llu shared_retested %llu\n",
+               "passes_time %llu passes %llu\n",
                g_tm[0], g_tm[1], g_tm[2], g_tm[3], g_tm[4], g_tm[5], g_tm[6], g_tm[7], g_tm[8], g_tm[9],
-               g_tm[10], g_tm[11], g_tm[12], g_tm[13], g_tm[14], g_tm[15]);
+               g_tm[10], g_tm[11], g_tm[12], g_tm[13]);
         for (int i = 0; i < 16; ++i) g_tm[i] = 0;
         g_tm_waves = 0;
     }

@@ -52,7 +52,6 @@ constexpr int RT_PIX_KEY = 1;  // queue kernels: the pixel's stream key from the
 constexpr int RT_START_BATCH = 1;  // sphere-only queue kernel: camera rays made 64 at a time, at full wave width, and handed out from LDS
 constexpr int RT_PACKET = 1;  // general queue kernel: camera rays of a wave traced as one packet (closest_packet)
 constexpr int RT_LEAF_REUSE = 1;  // cooperative search: a leaf whose ref list is the previous leaf's reuses its minimum
-constexpr int RT_SHARED = 1;  // cooperative search: refs the previous leaf held are tested only when needed (shared_mask)
 constexpr int RT_PACKET_MIN = 40;  // fewest camera rays of one direction octant that form a packet
 
 constexpr float EPS = 1e-4f;            // src/lib.rs:20
@@ -915,79 +914,6 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
     return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-// Mask of the refs of leaf list l (bit j: ref j, j < 32) that leaf list p also holds, 0 when the
-// pair has no entry (runtime.hip build_shared_masks).
-__device__ __forceinline__ uint32_t shared_mask(const DevScene& sc, uint32_t l, uint32_t p) {
-    const uint32_t h = shared_hash(l, p);
-    for (uint32_t q = 0; q < SHARED_PROBES; ++q) {
-        const uint4 e = sc.pair_tab[(h + q) & sc.pair_cap];
-        if (e.x == l && e.y == p) return e.z;
-        if (e.x == ~0u) break;
-    }
-    return 0;
-}
-
-// Position of the k-th set bit of m (k < popcount(m); any value otherwise).
-__device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t k) {
-    uint32_t pos = 0, c;
-    c = (uint32_t)__popc(m & 0xffffu);
-    if (k >= c) { k -= c; pos = 16; m >>= 16; }
-    c = (uint32_t)__popc(m & 0xffu);
-    if (k >= c) { k -= c; pos += 8; m >>= 8; }
-    c = (uint32_t)__popc(m & 0xfu);
-    if (k >= c) { k -= c; pos += 4; m >>= 4; }
-    c = (uint32_t)__popc(m & 0x3u);
-    if (k >= c) { k -= c; pos += 2; m >>= 2; }
-    return pos + (k >= (m & 1u) ? 1u : 0u);
-}
-
-// coop_leaf over a subset of each lane's leaf: the positions j < 32 with bit j of `sel` set, then
-// (tail) the positions 32 .. cnt - 1.  Keys as coop_leaf's (the index is the ref's position in
-// sc.refs), folded into key0.
-template <int PNT = 0>
-__device__ __forceinline__ unsigned long long coop_leaf_sel(const DevScene& sc, const Ray& r, uint32_t off,
-                                                            uint32_t cnt, uint32_t sel, bool tail, uint32_t lane,
-                                                            unsigned long long key0) {
-    const uint32_t nsel = (uint32_t)__popc(sel);
-    const uint32_t n = nsel + (tail && cnt > 32u ? cnt - 32u : 0u);
-    const uint32_t incl = wave_incl_scan(n, lane);
-    const uint32_t total = __shfl(incl, 63);
-    const uint32_t wbase = threadIdx.x & ~63u;
-    const uint32_t start = incl - n;
-    unsigned long long* const keys = coop_keys<PNT>();
-    __hip_atomic_store(&keys[threadIdx.x], key0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    for (uint32_t base = 0; base < total; base += 64) {
-        const uint32_t w = base + lane;
-        const uint32_t owner = pass_owner(incl, total, base, w);
-        const uint32_t k = w - __shfl(start, owner);
-        const uint32_t so = __shfl(sel, owner);
-        const uint32_t ns = (uint32_t)__popc(so);
-        const uint32_t idx = __shfl(off, owner) + (k < ns ? nth_bit(so, k) : 32u + (k - ns));
-        Ray ro;
-        ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
-        ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
-        if (w < total) {
-            const uint32_t ref = sc.refs[idx];
-            float4 a0, a1, a2;
-            if constexpr (PNT > 0) {
-                pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
-            } else {
-                const float4* pd = prim_data(sc, ref);
-                a0 = pd[0];
-                a1 = pd[1];
-                a2 = pd[2];
-            }
-            float l = 0.f, bu, bv;
-            bool h;
-            if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
-            else h = tri_hit(xyz(a0), xyz(a1), xyz(a2), ro, &l, &bu, &bv);
-            if (h && l >= HIT_MIN)  // valid and not NaN
-                atomicMin(&keys[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
-        }
-    }
-    return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
 // stack_search with cooperative leaves: the same per-lane traversal (kdtree.rs:66-104); lanes
 // whose search has ended (or that had no ray) keep looping as helpers until the wave is done.
 //
@@ -1042,7 +968,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     while (__ballot(!done) != 0) {
         uint32_t off = 0, cnt = 0, list = ~0u;
         unsigned long long key0 = ~0ull;
-        uint32_t skip = 0;  // RT_SHARED: bit j, ref j of the passes' part of the leaf, was in the previous leaf
         VC(12, 1);
         if (!done) {
             uint2 nd = fetch_node(sc, node);
@@ -1097,8 +1022,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 key0 = prev_key;
                 cnt = 0;
             } else {
-                // RT_SHARED: the refs the previous leaf also held (tested there, same ray)
-                if (RT_SHARED && !SLAB && (nd.x & LEAF_SHARED) && prev_list != ~0u) skip = shared_mask(sc, off, prev_list);
                 // The leaf's leading spheres (a scene's lights span most leaves) are this
                 // lane's own tests; the wave's passes then hold triangles only.
                 const uint32_t lead = nd.x >> LEAF_LEAD_SHIFT;
@@ -1113,27 +1036,11 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 }
                 off += lead;
                 cnt -= lead;
-                skip = lead < 32u ? skip >> lead : 0u;
             }
         }
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
-        unsigned long long key;
-        if (!RT_SHARED || SLAB || __ballot(skip != 0u) == 0) {
-            key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0), PNT>(sc, r, off, cnt, lane, key0);
-        } else {
-            // The refs not in the previous leaf first (the leading spheres are always tested).
-            // Every skipped ref was in the previous leaf, with this ray, so its length is at least
-            // that leaf's minimum (prev_key): with no hit there, none of them hits; a minimum below
-            // it is this leaf's.  Otherwise the skipped refs are tested too, and the leaf's first
-            // minimum is the full one.
-            key = coop_leaf_sel<PNT>(sc, r, off, cnt, ~skip & (cnt >= 32u ? ~0u : ((1u << cnt) - 1u)), true, lane, key0);
-            const bool rest = skip != 0u && prev_key != ~0ull &&
-                              !(key != ~0ull && (uint32_t)(key >> 32) < (uint32_t)(prev_key >> 32));
-            TM_ADD(14, __shfl(wave_incl_scan((uint32_t)__popc(skip), lane), 63));
-            TM_ADD(15, __shfl(wave_incl_scan(rest ? (uint32_t)__popc(skip) : 0u, lane), 63));
-            if (__ballot(rest)) key = coop_leaf_sel<PNT>(sc, r, off, cnt, rest ? skip : 0u, false, lane, key);
-        }
+        const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0), PNT>(sc, r, off, cnt, lane, key0);
         TM_ADD(12, TM_NOW() - tmc0);
         TM_ADD(13, (__shfl(wave_incl_scan(cnt, lane), 63) + 63u) / 64u);
         if (!done) {
