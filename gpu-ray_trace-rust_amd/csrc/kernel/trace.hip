@@ -941,6 +941,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     unsigned long long prev_key = ~0ull;
     // After a leaf that does not return: the reference's pop (or the kd-restart); false when the
     // interval is exhausted (the reference's empty stack).
+    // !RESTART: the pop after a leaf that does not return needs two nodes, the branch it returns to
+    // (its b word: children and axis) and the branch below it (the new exit); both are loaded ahead
+    // of the leaf's passes, so their trip to L1 / L2 overlaps the passes instead of following them
+    // (a380 and biplane +4..7%, spaceship +-0: the round's chain of dependent loads is the limiter)
+    uint32_t pop_b = 0;
+    uint2 below = make_uint2(0u, 0u);
     auto advance = [&]() -> bool {
         if (RESTART ? !pushed : sp == 0) return false;
         if (RESTART) {
@@ -949,15 +955,13 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             node = restart;
         } else {
             --sp;
-            VC(1, sp ? 2 : 1);
-            VL(1, sc.nodes + st[sp * BLOCK], 8, true);
-            const uint2 pn = fetch_node(sc, st[sp * BLOCK]);
+            // the popped branch's node and the one below it were loaded before the leaf's passes
             float d;
-            (void)split_t<FAST>(pn, ax, r, &d);
-            node = (pn.y >> 2) + (d > 0.0f ? 1u : 0u);
+            (void)split_t<FAST>(make_uint2(0u, pop_b), ax, r, &d);
+            node = (pop_b >> 2) + (d > 0.0f ? 1u : 0u);
             entry = top_t;
             if (sp) {
-                top_t = split_t<FAST>(fetch_node(sc, st[(sp - 1) * BLOCK]), ax, r, &d);
+                top_t = split_t<FAST>(below, ax, r, &d);
                 exit_t = top_t;
             } else {
                 exit_t = root_exit;
@@ -1037,6 +1041,12 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 off += lead;
                 cnt -= lead;
             }
+        }
+        if (!RESTART && !done && sp > 0) {  // the pop after this leaf (if it does not return)
+            VC(1, sp > 1 ? 2 : 1);
+            VL(1, sc.nodes + st[(sp - 1) * BLOCK], 8, true);
+            pop_b = fetch_node(sc, st[(sp - 1) * BLOCK]).y;
+            if (sp > 1) below = fetch_node(sc, st[(sp - 2) * BLOCK]);
         }
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
