@@ -944,7 +944,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     // !RESTART: the pop after a leaf that does not return needs two nodes, the branch it returns to
     // (its b word: children and axis) and the branch below it (the new exit); both are loaded ahead
     // of the leaf's passes, so their trip to L1 / L2 overlaps the passes instead of following them
-    // (a380 and biplane +4..7%, spaceship +-0: the round's chain of dependent loads is the limiter)
+    // (A/B at 4-10 spp: a380 and biplane +4..7%, spaceship +-0; the bench configs +-0)
     uint32_t pop_b = 0;
     uint2 below = make_uint2(0u, 0u);
     auto advance = [&]() -> bool {
