@@ -4,7 +4,6 @@
 // (src/render/draw_scene.rs:17-47).  Host float work here (RayCompute) is compiled with
 // -ffp-contract=off, like the oracle.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <atomic>
@@ -131,14 +130,6 @@ struct rt_ctx {
     uint32_t grid_div = 0;        // RT_DEBUG_GRID_DIV; 0: small_grid_div(the launch's slots)
     uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_DEBUG_QUEUE_SHARDS)
     uint64_t group_items = 0;     // rt_render_to_target: samples per batch group (RT_DEBUG_GROUP_ITEMS; 0: GROUP_ITEMS)
-    // RT_DEBUG_SCHED=wave (experiment): the wavefront schedule's buffers (run_wave)
-    bool wave = false;
-    uint32_t wave_cap = 0;
-    WfPath* wf_paths = nullptr;
-    uint32_t* wf_buf = nullptr;       // idx a, idx b, keys a, keys b (wave_cap each), then the count
-    void* wf_temp = nullptr;
-    size_t wf_temp_bytes = 0;
-    uint32_t* wf_count_host = nullptr;
     float last_ms = 0.f;
     std::string err;
 };
@@ -336,10 +327,6 @@ static void destroy_ctx(rt_ctx* c) {
         if (sl.fold_done) (void)hipEventDestroy(sl.fold_done);
         if (sl.stream) (void)hipStreamDestroy(sl.stream);
     }
-    if (c->wf_paths) (void)hipFree(c->wf_paths);
-    if (c->wf_buf) (void)hipFree(c->wf_buf);
-    if (c->wf_temp) (void)hipFree(c->wf_temp);
-    if (c->wf_count_host) (void)hipHostFree(c->wf_count_host);
     for (hipEvent_t e : c->lev) (void)hipEventDestroy(e);
     if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
     if (c->win_end_ev) (void)hipEventDestroy(c->win_end_ev);
@@ -587,22 +574,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         for (uint32_t i = 0; i < scene->n_spheres; ++i) pool[3 * (size_t)i] = sph[i];
         std::memcpy(pool.data() + 3 * (size_t)scene->n_spheres, ftri.data(), ftri.size() * sizeof(float4));
         if (n_mesh) std::memcpy(pool.data() + 3 * ((size_t)scene->n_spheres + scene->n_free_tris), mf.verts.data(), 3 * n_mesh * sizeof(float4));
-        {   // the wavefront schedule's origin cells: the triangles' box (the root box without any)
-            float lo[3] = {tree->bounds[0], tree->bounds[2], tree->bounds[4]};
-            float hi[3] = {tree->bounds[1], tree->bounds[3], tree->bounds[5]};
-            if (pool.size() / 3 > scene->n_spheres) {
-                for (int k = 0; k < 3; ++k) lo[k] = INFINITY, hi[k] = -INFINITY;
-                for (size_t q = 3 * (size_t)scene->n_spheres; q < pool.size(); ++q) {
-                    const float v[3] = {pool[q].x, pool[q].y, pool[q].z};
-                    for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], v[k]), hi[k] = std::max(hi[k], v[k]);
-                }
-            }
-            for (int k = 0; k < 3; ++k) {
-                d.wf_lo[k] = std::isfinite(lo[k]) ? lo[k] : 0.f;
-                const float ext = hi[k] - lo[k];
-                d.wf_scale[k] = std::isfinite(ext) && ext > 0.f ? 511.0f / ext : 0.f;
-            }
-        }
         // triangles as {v0, e1 = v1 - v0, e2 = v2 - v0}: generic.rs:104-105's edges, the same f32
         // subtractions the device would make per test
         for (size_t t = scene->n_spheres; t < pool.size() / 3; ++t) {
@@ -723,10 +694,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     if (const char* e = debug_env("SCHED")) {
         if (!std::strcmp(e, "direct")) c->sched = 1;
         else if (!std::strcmp(e, "queue")) c->sched = 2;
-        else if (!std::strcmp(e, "wave")) c->wave = true;  // general scenes only (run_wave)
     }
-    d.wf_mode = 1u;
-    if (const char* e = debug_env("WAVE_MODE")) d.wf_mode = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = debug_env("LANES_PER_PIXEL")) {
         unsigned long v = std::strtoul(e, nullptr, 10);
         if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
@@ -1062,60 +1030,6 @@ static bool use_queue(const rt_ctx* c) {
 // ([sample][pixel], so a part is a contiguous block) and continues the running mean exactly where
 // the previous part left it: the frames are those of one call per batch, bit for bit.  Chunks of
 // a call with several batches hold whole batches when a batch fits the radiance cap.
-// Wavefront schedule (RT_DEBUG_SCHED=wave, an experiment; trace.hip wf_bounce_kernel): the
-// launch's items in batches of wave_cap paths; each batch is traced one bounce at a time, the
-// continuing paths sorted by (direction octant, origin cell) between bounces.  Synchronous: the
-// host reads the count of continuing paths after every bounce.
-constexpr uint32_t WAVE_CAP = 1u << 22;
-static int run_wave(rt_ctx* c, LaunchArgs a, hipStream_t s) {
-    const uint32_t cap = WAVE_CAP;
-    if (c->wave_cap < cap) {
-        if (c->wf_paths) (void)hipFree(c->wf_paths);
-        if (c->wf_buf) (void)hipFree(c->wf_buf);
-        if (c->wf_temp) (void)hipFree(c->wf_temp);
-        c->wf_paths = nullptr;
-        c->wf_buf = nullptr;
-        c->wf_temp = nullptr;
-        c->wave_cap = 0;
-        if (hipMalloc(&c->wf_paths, (size_t)cap * sizeof(WfPath)) != hipSuccess ||
-            hipMalloc(&c->wf_buf, (4 * (size_t)cap + 16) * sizeof(uint32_t)) != hipSuccess)
-            return set_err(c, RT_ERR_OOM, "wavefront buffers");
-        size_t tb = 0;
-        HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cap, 0, 30, s));
-        if (hipMalloc(&c->wf_temp, tb) != hipSuccess) return set_err(c, RT_ERR_OOM, "wavefront sort buffer");
-        c->wf_temp_bytes = tb;
-        if (!c->wf_count_host && hipHostMalloc(&c->wf_count_host, 64) != hipSuccess)
-            return set_err(c, RT_ERR_OOM, "wavefront count");
-        c->wave_cap = cap;
-    }
-    uint32_t* idx_a = c->wf_buf;
-    uint32_t* idx_b = idx_a + cap;
-    uint32_t* key_a = idx_b + cap;
-    uint32_t* key_b = key_a + cap;
-    uint32_t* count = key_b + cap;
-    for (uint32_t item0 = 0; item0 < a.n_items; item0 += cap) {
-        const uint32_t n = a.n_items - item0 < cap ? a.n_items - item0 : cap;
-        HIPCHK(c, launch_wf_gen(a, item0, n, c->wf_paths, idx_a, s));
-        uint32_t live = n;
-        while (live) {
-            HIPCHK(c, hipMemsetAsync(count, 0, sizeof(uint32_t), s));
-            HIPCHK(c, launch_wf_bounce(a, c->wf_paths, idx_a, live, idx_b, key_b, count, s));
-            HIPCHK(c, hipMemcpyAsync(c->wf_count_host, count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            live = *c->wf_count_host;
-            if (!live) break;
-            if (a.sc.wf_mode & 2u) {
-                std::swap(idx_a, idx_b);
-                continue;
-            }
-            size_t tb = c->wf_temp_bytes;
-            HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->wf_temp, tb, key_b, key_a, idx_b, idx_a, (int)live, 0, 30, s));
-        }
-    }
-    return RT_OK;
-}
-
 static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sample_begin,
                          uint32_t sample_count, hipEvent_t after, uint32_t batch, float4* const* outs) {
     if (batch == 0 || batch > sample_count) batch = sample_count ? sample_count : 1u;
@@ -1203,11 +1117,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
             uint32_t nb = (uint32_t)(lanes / tpb);
             if (overlap && small && busy && grid_div > 1)
                 nb = nb / grid_div > (uint32_t)c->n_cu ? nb / grid_div : (uint32_t)c->n_cu;
-            if (c->wave && !a.sc.spheres_only && !a.sc.dls) {
-                if ((st = run_wave(c, a, sl.stream))) return st;
-            } else {
-                HIPCHK(c, launch_trace_queue(a, nb, sl.stream));
-            }
+            HIPCHK(c, launch_trace_queue(a, nb, sl.stream));
             if ((st = record_launch_event(c, false, sl.stream))) return st;
         }
         if (c->last_fold && c->last_fold != sl.fold_done) HIPCHK(c, hipStreamWaitEvent(sl.stream, c->last_fold, 0));

@@ -79,10 +79,6 @@ struct DevScene {
     // launch; pool_nt = its threads per workgroup (768 / 1024), 0 = off; n_pool = primitives.
     uint32_t pool_nt;
     uint32_t n_pool;
-    // wavefront schedule (RT_DEBUG_SCHED=wave): the sort key's origin cells, Morton over the
-    // leaf-testable primitives' box (wf_lo, 511 / extent per axis)
-    float wf_lo[3], wf_scale[3];
-    uint32_t wf_mode;  // RT_DEBUG_WAVE_MODE bits: 1 packets for every ray (not just camera rays), 2 no sort
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r
@@ -187,11 +183,6 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_count(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_fold(const LaunchArgs& a, hipStream_t s);
 hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_t s);
-struct WfPath { float4 a, b, c, d; };  // a wavefront path: {o, depth} {d, slot} {L, rng lo} {T, rng hi}
-hipError_t launch_wf_gen(const LaunchArgs& a, uint32_t item0, uint32_t n, WfPath* paths, uint32_t* order,
-                         hipStream_t s);
-hipError_t launch_wf_bounce(const LaunchArgs& a, WfPath* paths, const uint32_t* order, uint32_t n, uint32_t* next_idx,
-                            uint32_t* next_keys, uint32_t* next_n, hipStream_t s);
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks);
 size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks);  // 0: the stack is in LDS
 uint32_t queue_block_threads(const LaunchArgs& a);  // threads per workgroup of the scene's queue kernel

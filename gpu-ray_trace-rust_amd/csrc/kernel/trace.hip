@@ -2096,136 +2096,6 @@ __global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) v
     }
 }
 
-static size_t stack_lds_bytes(const LaunchArgs& a);
-// ---------------------------------------------------------------- wavefront schedule (experiment)
-// RT_DEBUG_SCHED=wave: the launch's items traced bounce by bounce instead of by persistent lanes.
-// A batch of paths lives in HBM (WfPath, 64 B); each bounce traces every live path one segment
-// (wf_bounce_kernel: the segment() of the queue kernel, packets allowed for every ray), and the
-// paths that continue are sorted by direction octant and origin cell (runtime.hip, hipcub radix
-// sort) so that a wave's rays start together and point the same way.  Each path's arithmetic is
-// the queue kernel's, only its lane and its time change, so the images are the same bit for bit.
-__device__ __forceinline__ uint32_t wf_spread10(uint32_t x) {  // 9 bits -> every third bit
-    x &= 0x1ffu;
-    x = (x | (x << 16)) & 0x030000ffu;
-    x = (x | (x << 8)) & 0x0300f00fu;
-    x = (x | (x << 4)) & 0x030c30c3u;
-    x = (x | (x << 2)) & 0x09249249u;
-    return x;
-}
-// the sort key of a path about to trace `r` (d not yet normalized): octant << 27 | Morton(o)
-__device__ __forceinline__ uint32_t wf_key(const DevScene& sc, const Ray& r) {
-    const uint32_t oct = (r.d.x > 0.0f ? 1u : 0u) | (r.d.y > 0.0f ? 2u : 0u) | (r.d.z > 0.0f ? 4u : 0u);
-    auto q = [](float v, float lo, float s) {
-        const float t = (v - lo) * s;
-        return t > 0.0f ? (t < 511.0f ? (uint32_t)t : 511u) : 0u;  // NaN -> 0
-    };
-    const uint32_t m = wf_spread10(q(r.o.x, sc.wf_lo[0], sc.wf_scale[0])) |
-                       (wf_spread10(q(r.o.y, sc.wf_lo[1], sc.wf_scale[1])) << 1) |
-                       (wf_spread10(q(r.o.z, sc.wf_lo[2], sc.wf_scale[2])) << 2);
-    return (oct << 27) | m;
-}
-__device__ __forceinline__ void wf_store(WfPath* w, const Path& p, uint32_t slot) {
-    w->a = make_float4(p.ray.o.x, p.ray.o.y, p.ray.o.z, __int_as_float(p.depth));
-    w->b = make_float4(p.ray.d.x, p.ray.d.y, p.ray.d.z, __uint_as_float(slot));
-    w->c = make_float4(p.L.x, p.L.y, p.L.z, __uint_as_float((uint32_t)p.rng));
-    w->d = make_float4(p.T.x, p.T.y, p.T.z, __uint_as_float((uint32_t)(p.rng >> 32)));
-}
-// paths[i] for items item0 + i, i < n; order[i] = i (bounce 0 keeps the queue's pixel order)
-__global__ __launch_bounds__(256) void wf_gen_kernel(LaunchArgs a, uint32_t item0, uint32_t n, WfPath* paths,
-                                                     uint32_t* order) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    const DevScene& sc = a.sc;
-    const uint32_t item = item0 + i;
-    uint32_t j, o;
-    split_item(a, item, &j, &o);
-    int x, y;
-    uint64_t key;
-    if (a.pix_q) {
-        const uint4 e = a.pix_q[o];
-        x = (int)(e.x & 0xffffu);
-        y = (int)(e.x >> 16);
-        o = e.y;
-        key = RT_PIX_KEY ? ((uint64_t)e.w << 32) | e.z : rt_rng_pixel_key(sc.seed, (uint32_t)y * sc.width + (uint32_t)x);
-    } else {
-        launch_pixel(a, o, &x, &y);
-        key = rt_rng_pixel_key(sc.seed, (uint32_t)y * sc.width + (uint32_t)x);
-    }
-    Path p;
-    start_path(sc, p, camera_base_dir(sc, x, y), key, a.sample_begin + j);
-    wf_store(paths + i, p, j * a.n_pix + o);
-    order[i] = i;
-}
-// One segment of the paths order[0 .. n): the ended ones write their radiance, the others are
-// stored back and appended (index, sort key) to next_idx / next_keys.
-template <bool RESTART>
-__global__ __launch_bounds__(BLOCK, RT_MIN_WAVES_GEN) void wf_bounce_kernel(LaunchArgs a, WfPath* paths,
-                                                                            const uint32_t* order, uint32_t n,
-                                                                            uint32_t* next_idx, uint32_t* next_keys,
-                                                                            uint32_t* next_n) {
-    extern __shared__ uint32_t dyn_lds[];
-    const DevScene& sc = a.sc;
-    uint32_t* st = dyn_lds + threadIdx.x;
-    Ctr<false> c;
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    const bool have = i < n;
-    const uint32_t pi = have ? order[i] : 0u;
-    Path p;
-    uint32_t slot = 0;
-    {
-        const WfPath w = paths[pi];
-        p.ray.o = mk(w.a.x, w.a.y, w.a.z);
-        p.depth = __float_as_int(w.a.w);
-        p.ray.d = mk(w.b.x, w.b.y, w.b.z);
-        slot = __float_as_uint(w.b.w);
-        p.L = mk(w.c.x, w.c.y, w.c.z);
-        p.T = mk(w.d.x, w.d.y, w.d.z);
-        p.rng = ((uint64_t)__float_as_uint(w.d.w) << 32) | __float_as_uint(w.c.w);
-        p.dls_on = false;
-    }
-    const PkScene ps{sc.nodes, sc.refs, sc.prim4};
-    p.ray.d = normalize(p.ray.d);
-    Hit h;
-    const bool hit = closest_coop<RESTART, false, 0>(sc, p.ray, &h, st, have, (sc.wf_mode & 1u) || p.depth == 0, &ps);
-    bool fin = false;
-    if (have) fin = shade<false, true, false>(sc, p, h, hit, c);
-    if (have && fin) {
-        float* r = a.radiance + 3 * (size_t)slot;
-        r[0] = p.L.x;
-        r[1] = p.L.y;
-        r[2] = p.L.z;
-    }
-    const bool cont = have && !fin;
-    if (cont) wf_store(paths + pi, p, slot);
-    // append the continuing paths, one atomic per wave
-    const uint64_t m = __ballot(cont);
-    uint32_t base = 0;
-    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)m) - 1) && m)
-        base = atomicAdd(next_n, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)(__ffsll((unsigned long long)m) - 1) & 63);
-    if (cont) {
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        next_idx[base + r] = pi;
-        next_keys[base + r] = wf_key(sc, p.ray);
-    }
-}
-hipError_t launch_wf_gen(const LaunchArgs& a, uint32_t item0, uint32_t n, WfPath* paths, uint32_t* order,
-                         hipStream_t s) {
-    hipLaunchKernelGGL(wf_gen_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, item0, n, paths, order);
-    return hipGetLastError();
-}
-hipError_t launch_wf_bounce(const LaunchArgs& a, WfPath* paths, const uint32_t* order, uint32_t n, uint32_t* next_idx,
-                            uint32_t* next_keys, uint32_t* next_n, hipStream_t s) {
-    const size_t lds = a.sc.restart ? 0 : stack_lds_bytes(a);
-    if (a.sc.restart)
-        hipLaunchKernelGGL(wf_bounce_kernel<true>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds, s, a, paths, order, n,
-                           next_idx, next_keys, next_n);
-    else
-        hipLaunchKernelGGL(wf_bounce_kernel<false>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), lds, s, a, paths, order, n,
-                           next_idx, next_keys, next_n);
-    return hipGetLastError();
-}
-
 // Running mean over the traced chunk, in sample order (draw_scene.rs:81-83): one lane per
 // launch pixel; reads are coalesced across lanes ([sample][pixel] layout).
 __global__ __launch_bounds__(256) void fold_kernel(LaunchArgs a) {
