@@ -110,3 +110,60 @@ def test_adversarial_triangles_bit_exact(gpu_available, oracle, monkeypatch, see
         with render.Context(sc) as c:
             g = c.render(tiles, 0, 4)
         assert np.array_equal(g, o), (env, parity.stats(g, o))
+
+
+def _axis_aligned_triangles(seed: int) -> dict:
+    """Unit cubes on an integer grid, each face two triangles: every triangle lies in an
+    axis-aligned plane through integer coordinates, neighbouring cubes share faces (exact
+    duplicates, opposite normals) and edges, and the camera looks down an axis, so primary rays
+    have zero direction components (the reference's EPS clamp, kdtree.rs:75) and hit edges,
+    corners and split planes exactly."""
+    rng = np.random.default_rng(2000 + seed)
+    mats = [{"divert_ray": "Diff"}, {"divert_ray": "Spec"}, {"divert_ray": {"!DiffSpec": {"diffp": 0.5}}}]
+    members = []
+    cells = {tuple(int(x) for x in rng.integers(-3, 3, 3)) for _ in range(9)}
+    for (x, y, z) in sorted(cells):
+        m = mats[int(rng.integers(0, 3))]
+        rgb = rng.uniform(0.3, 0.95, 3)
+        for ax in range(3):
+            for side in (0, 1):
+                o1, o2 = (ax + 1) % 3, (ax + 2) % 3
+                q = np.zeros((4, 3))
+                for k, (s1, s2) in enumerate(((0, 0), (1, 0), (1, 1), (0, 1))):
+                    q[k, ax], q[k, o1], q[k, o2] = side, s1, s2
+                q += np.array([x, y, z], np.float64)
+                members.append(_tri([q[0], q[1], q[2]], m, rgb))
+                members.append(_tri([q[0], q[2], q[3]], m, rgb))
+    members.append({"!Sphere": {"c": [0.0, 0.0, 0.0], "r": 40.0, "coloring": {"!Solid": [0.0, 0.0, 0.0]},
+                                "mat": {"divert_ray": "Diff", "emissive": [0.9, 0.8, 0.7]}}})
+    ax = seed % 3
+    o = [0.0, 0.0, 0.0]
+    o[ax] = 9.0
+    d = [0.0, 0.0, 0.0]
+    d[ax] = -4.0
+    up = [0, 1, 0] if ax != 1 else [0, 0, 1]
+    return {"cam": {"d": d, "o": o, "screen_height": 4.0, "screen_width": 6.0, "up": up, "view_eulers": [0, 0, 0]},
+            "render_info": {"gpu_render_batch": 1, "height": 96, "width": 144, "kd_tree_depth": 17,
+                            "rad_info": {"debug_single_ray": False, "dir_light_samp": False,
+                                         "russ_roull_info": {"assured_depth": 3, "max_thres": 0.5}},
+                            "samps_per_pix": 4, "use_gpu": True},
+            "scene_members": members}
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_axis_aligned_triangles_bit_exact(gpu_available, oracle, monkeypatch, seed):
+    import parity
+    from rt_amd import render, scheme
+
+    sc = scheme.load(_axis_aligned_triangles(seed))
+    tiles = [(0, 0, 144, 96)]
+    o = oracle.render(sc, tiles, 0, 4, accum=oracle.ACCUM_FORWARD)
+    assert np.isfinite(o).all() and (o[:, :3].sum(1) > 0).mean() > 0.99
+    for env in ({}, {"RT_DEBUG_KD_RESTART": "1"}, {"RT_DEBUG_PACKET": "0"}):
+        for k in ("RT_DEBUG_KD_RESTART", "RT_DEBUG_PACKET"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with render.Context(sc) as c:
+            g = c.render(tiles, 0, 4)
+        assert np.array_equal(g, o), (env, parity.stats(g, o))
