@@ -9,8 +9,9 @@ the oracle, on triangle sets built to make the closest-hit decision hard
 - light spheres among them and an emissive sphere around all of it, so full paths bounce
   between the triangles (diffuse, DiffSpec, mirror and dielectric materials) and every pixel's
   value carries every hit of its paths.
-Whole paths, forward accumulation (the device's order): bit-exact, for the stack
-and the stackless traversal and with camera-ray packets off."""
+Whole paths, forward accumulation (the device's order), half of the scenes through a
+thin-lens camera: bit-exact, for the stack and the stackless traversal and with camera-ray packets
+off."""
 import numpy as np
 import pytest
 
@@ -83,8 +84,11 @@ def _adversarial_triangles(seed: int) -> dict:
     o = rng.uniform(-4.0, 4.0, 3) if seed % 2 == 0 else np.array([0.0, 0.0, 7.5])
     d = rng.normal(size=3) if seed % 2 == 0 else np.array([0.0, 0.0, -1.0])
     d = 5.0 * d / np.linalg.norm(d)
-    return {"cam": {"d": [float(x) for x in d], "o": [float(x) for x in o], "screen_height": 5.0,
-                    "screen_width": 8.0, "up": [0, 1, 0], "view_eulers": [0, 0, 0]},
+    cam = {"d": [float(x) for x in d], "o": [float(x) for x in o], "screen_height": 5.0,
+           "screen_width": 8.0, "up": [0, 1, 0], "view_eulers": [0, 0, 0]}
+    if seed >= 4:
+        cam["lens_r"] = 0.05  # a thin lens: camera rays from different origins (generate.rs:39-66)
+    return {"cam": cam,
             "render_info": {"gpu_render_batch": 1, "height": 96, "width": 160, "kd_tree_depth": 17,
                             "rad_info": {"debug_single_ray": False, "dir_light_samp": False,
                                          "russ_roull_info": {"assured_depth": 3, "max_thres": 0.5}},
