@@ -294,9 +294,9 @@ static uint32_t queue_shards(uint32_t n_spheres, uint32_t n_free_tris, size_t n_
     const uint64_t n = (uint64_t)n_spheres + n_free_tris + n_mesh_tris;
     if ((n_free_tris + n_mesh_tris) > 0 && n <= 64) return 8u;
     // Scenes too large for one XCD's 4 MB L2 (a380: 127 K triangles, ~10 MB of nodes and
-    // primitives): each XCD works on its own shard of the launch's pixels (a wave starts on shard
-    // blockIdx % 8, and workgroups are dealt to the XCDs round-robin), so its L2 holds the
-    // geometry of its own part of the frame.  a380 +1.6% in the bench's config shape, +4..11% in
+    // primitives): each XCD walks its own shard of the launch's items (a wave starts on shard
+    // blockIdx % 8, and workgroups are dealt to the XCDs round-robin), so its waves are on a
+    // window of pixels of their own and its L2 holds a smaller window's geometry.  a380 +1.6% in the bench's config shape, +4..11% in
     // synchronous launches; biplane and spaceship keep one counter (shards cost them 3%).
     if (n >= (1u << 16)) return 8u;
     return 1u;
