@@ -109,7 +109,7 @@ struct rt_ctx {
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
     uint4* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
     uint32_t pix_block = 1;           // RT_DEBUG_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
-    uint32_t pix_order = 0;           // RT_DEBUG_PIX_ORDER (experiment): 0 raster, 1 reverse, 2 centre first
+    uint32_t pix_order = 0;           // RT_DEBUG_PIX_ORDER (experiment): 0 raster, 1 reverse, 2 centre first, 3 Morton
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
     float4* d_out = nullptr;
@@ -938,7 +938,15 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                            (pq[b1].x >> 16) / B == (xy >> 16) / B)
                         ++b1;
                     const double dx = (double)(xy & 0xffffu) - 0.5 * c->sc.width, dy = (double)(xy >> 16) - 0.5 * c->sc.height;
-                    key.push_back({c->pix_order == 1 ? -(double)b0 : dx * dx + dy * dy, b0});
+                    double k = c->pix_order == 1 ? -(double)b0 : dx * dx + dy * dy;
+                    if (c->pix_order == 3) {  // Morton order of the blocks: a compact 2-D window in flight
+                        uint64_t m = 0;
+                        const uint32_t bx = (xy & 0xffffu) / B, by = (xy >> 16) / B;
+                        for (int bit = 0; bit < 16; ++bit)
+                            m |= (uint64_t)((bx >> bit) & 1u) << (2 * bit) | (uint64_t)((by >> bit) & 1u) << (2 * bit + 1);
+                        k = (double)m;
+                    }
+                    key.push_back({k, b0});
                     b0 = b1;
                 }
                 std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
