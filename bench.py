@@ -67,8 +67,9 @@ def self_launch_cmd(argv, env, port):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config-only", default=None)
     ap.add_argument("--as-rank", default=None)
+    ap.add_argument("--frame-abi", action="store_true")
     known, _ = ap.parse_known_args(argv)
-    if "WORLD_SIZE" in env or known.gpus <= 1 or known.config_only or known.as_rank:
+    if "WORLD_SIZE" in env or known.gpus <= 1 or known.config_only or known.as_rank or known.frame_abi:
         return None
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(known.gpus),
             "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
@@ -400,7 +401,10 @@ def run_config(name, cpu, build_id, per_batch_calls=True):
     w, h = int(loaded.info.width), int(loaded.info.height)
     tiles = [(0, 0, w, h)]
     nb = total // batch
-    group_items = int(os.environ.get("RT_DEBUG_GROUP_ITEMS") or GROUP_ITEMS)  # as rt_render_to_target reads it
+    group_items = GROUP_ITEMS  # as rt_render_to_target reads it (RT_DEBUG_LAUNCH group_items overrides)
+    for kv in os.environ.get("RT_DEBUG_LAUNCH", "").split(","):
+        if kv.startswith("group_items="):
+            group_items = int(kv.split("=", 1)[1])
     group = max(1, min(nb, group_items // (w * h * batch)))
     res = {"workload": f"{scene}.yml {w}x{h}, {total} spp in batches of {batch}, kd_tree_depth "
                        f"{int(loaded.info.kd_tree_depth)}; {nb} batches per run, each batch's frame in its own "
@@ -479,6 +483,83 @@ def config_at_queues(name, queues):
     return {k: d[k] for k in ("value", "value_per_batch_calls", "hw_queues") if k in d}
 
 
+def device_identity(rank, local):
+    """Which GPU this rank runs on: its device ordinal, PCI location (domain:bus:device, as
+    hipDeviceGetPCIBusId prints it) and UUID, so an N-rank line shows the ranks on N devices."""
+    import torch
+
+    p = torch.cuda.get_device_properties(local)
+    return {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": local,
+            "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0",
+            "uuid": str(getattr(p, "uuid", "")), "name": p.name,
+            "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+
+
+def gather_identities(ident, dist, world):
+    """Every rank's device_identity, on every rank (all_gather_object over the process group)."""
+    if dist is None:
+        return [ident]
+    out = [None] * world
+    dist.all_gather_object(out, ident)
+    return out
+
+
+def rank_summary(idents, dist):
+    """The N-rank line's proof of what ran: each rank's device and PCI location, how many distinct
+    devices they were, and the process group's backend and size."""
+    r = {"ranks": idents, "distinct_devices": len({i["pci_bus_id"] + i["uuid"] for i in idents})}
+    if dist is not None:
+        r["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+    return r
+
+
+def frame_abi_run(loaded, devices, spp, steps, warmup, digest=False):
+    """The C-ABI multi-device frame (rt_frame_*, frame.hip) in THIS process: one context per entry
+    of `devices` (each renders its stripes, the deal of rt_stripe_tiles), `warmup` untimed steps,
+    then exactly `steps` steps of `spp` samples over the whole frame (strong scaling: the contexts
+    split each step's W*H*spp samples) and ONE gather at the frame's end (peer copies to devices[0],
+    then one placement per context), synchronized on every device before and after.  This is the
+    path the reference's render thread (renderer.rs:43-60) would call; bench.py's torch ranks
+    measure the same split with one process per GPU."""
+    import hashlib
+
+    import torch
+
+    from rt_amd import render
+
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    with render.Frame(loaded, devices) as f:
+        s0 = 0
+        for _ in range(warmup):
+            f.render(s0, spp)
+            s0 += spp
+        f.gather(want_host=False)
+        f.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            f.render(s0, spp)
+            s0 += spp
+        f.gather(want_host=False)  # the frame-end gather (returns once the frame is placed)
+        f.synchronize()
+        dt = time.perf_counter() - t0
+        st = f.stats()
+        out = {"value": round(w * h * spp * steps / dt / 1e6, 3), "unit": "Msamples/s",
+               "ms_per_step": round(dt / steps * 1e3, 3), "devices": list(devices),
+               "pci_bus_ids": [device_identity(0, d)["pci_bus_id"] for d in sorted(set(devices))],
+               "stripe_rows": st["stripe_rows"], "gathers_timed": 1,
+               "peer_copy_ms_max": round(st["peer_copy_ms_max"], 3), "place_ms": round(st["place_ms"], 3),
+               "render_ms_max": round(st["render_ms_max"], 3), "n_peer_copies": st["n_peer_copies"],
+               "n_parts": st["n_parts"],
+               "note": "rt_frame_* in one process (C ABI, frame.hip): one context per device, one gather per frame "
+                       "(hipMemcpyPeerAsync to the first device + one strided placement per context)"}
+        if digest:
+            frame = f.gather(want_host=True)  # after the timed region
+            out["frame_sha256"] = hashlib.sha256(frame.tobytes()).hexdigest()
+            out["frame_complete"] = bool((frame[..., 3] == 1.0).all())
+    torch.cuda.synchronize()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -511,6 +592,13 @@ def main():
     ap.add_argument("--gather", default="frame", choices=("frame", "step"),
                     help="N > 1: gather the ranks' tiles once at frame end (north_star; default) or after every "
                          "step (the reference's per-batch read-back); the other mode is reported beside it")
+    ap.add_argument("--frame-abi", action="store_true",
+                    help="time the C-ABI multi-device frame (rt_frame_*: one process, one context per device, "
+                         "one gather per frame) as the headline instead of torch ranks; --gpus N contexts")
+    ap.add_argument("--frame-devices", default=None,
+                    help="comma-separated device ordinals of the --frame-abi contexts (default 0..N-1; tests: 0,0)")
+    ap.add_argument("--no-frame-abi", action="store_true",
+                    help="N > 1 torch ranks: skip rank 0's C-ABI frame leg over the ranks' devices")
     ap.add_argument("--config-only", default=None, choices=sorted(CONFIGS),
                     help="print one BASELINE config's JSON (no CPU leg) and exit: bench's child for the "
                          "4-queue a380 figure")
@@ -522,6 +610,8 @@ def main():
         return
     if args.same_device and args.dist_backend != "gloo":
         raise SystemExit("--same-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
+    if args.frame_abi:
+        return main_frame_abi(args)
 
     import torch
 
@@ -542,6 +632,8 @@ def main():
 
     from rt_amd import abi, render
 
+    # every rank's device, gathered to rank 0: the line shows which GPUs the N ranks ran on
+    idents = gather_identities(device_identity(rank, local), dist, world)
     sch, loaded = load(args.scene, args.width, args.height)
     w, h = int(loaded.info.width), int(loaded.info.height)
     spp = args.spp_per_step or int(sch["render_info"].get("gpu_render_batch") or 1)
@@ -610,6 +702,7 @@ def main():
                       "parallelism": f"tiles{world}", "dispatch": "sync" if args.sync else "async",
                       "dist_backend": args.dist_backend if world > 1 else None}}
     res["frame_complete"] = frame_complete
+    res.update(rank_summary(idents, dist))
     if frame_sha:
         res["frame_sha256"] = frame_sha
     res["launcher"] = (os.environ.get("RT_BENCH_LAUNCHER") or "torch.distributed.run") if world > 1 else None
@@ -650,6 +743,17 @@ def main():
         del fw
     elif not args.as_rank:
         res["weak"] = {"value": res["value"], "note": "N = 1: weak and strong scaling are the same run"}
+    if world > 1 and not args.no_frame_abi:
+        # the same strong split through the C ABI (rt_frame_*): rank 0 alone, one context on each
+        # rank's device, while the other ranks wait at a barrier
+        dist.barrier()
+        if rank == 0:
+            try:
+                res["frame_abi"] = frame_abi_run(loaded, [i["device"] for i in idents], spp, args.steps,
+                                                 args.warmup, digest=args.frame_digest)
+            except Exception as e:  # reported, never fatal to the torch-rank headline
+                res["frame_abi"] = {"error": repr(e)[:300]}
+        dist.barrier()
 
     build_id = abi.kernel_build_id()
     if rank == 0 and not args.no_roofline:
@@ -706,6 +810,36 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(res), flush=True)
+
+
+def main_frame_abi(args):
+    """`--frame-abi`: the headline is the C-ABI multi-device frame in one process (no torch ranks,
+    no launcher): --gpus N contexts on --frame-devices (default 0..N-1), strong scaling."""
+    import torch
+
+    from rt_amd import abi
+
+    devices = ([int(d) for d in args.frame_devices.split(",")] if args.frame_devices else list(range(args.gpus)))
+    if len(devices) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but {len(devices)} --frame-devices")
+    torch.cuda.set_device(devices[0])
+    sch, loaded = load(args.scene, args.width, args.height)
+    w, h = int(loaded.info.width), int(loaded.info.height)
+    spp = args.spp_per_step or int(sch["render_info"].get("gpu_render_batch") or 1)
+    r = frame_abi_run(loaded, devices, spp, args.steps, args.warmup, digest=args.frame_digest)
+    res = {"metric": f"Msamples/s (pixels x spp / s) on {args.scene}.yml", "value": r["value"], "unit": "Msamples/s",
+           "n_gpus": args.gpus, "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
+           "bench_schema": 4, "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic-free: the reference's own scene file (tests/golden/scenes), seeded RNG",
+           "config": {"workload": f"{args.scene}.yml {w}x{h}, {spp} spp per step, split over {args.gpus} "
+                                  f"contexts of one process (rt_frame_*)", "spp_per_step": spp, "pixels": w * h,
+                      "parallelism": f"frame_abi{args.gpus}", "dispatch": "async"},
+           "frame_abi": r, "ranks": [device_identity(0, d) for d in devices],
+           "distinct_devices": len(set(devices)), "build_id": abi.kernel_build_id()}
+    if "frame_sha256" in r:
+        res["frame_sha256"] = r["frame_sha256"]
+        res["frame_complete"] = r["frame_complete"]
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -39,7 +40,8 @@ struct Part {                    // one context: its device, stripes and buffers
     std::vector<rt_tile> tiles;
     uint64_t npix = 0;
     float* buf = nullptr;        // tiles concatenated, RGBA f32, on `device`
-    float* staging = nullptr;    // on the first device, when `device` is another one
+    bool remote = false;         // gathered through staging: on another device (or RT_DEBUG_FRAME_STAGING)
+    float* staging = nullptr;    // on the first device, when remote
     hipStream_t stream = nullptr;   // on `device`: the context's caller stream, the peer copy
     hipEvent_t copied = nullptr;    // on `stream`: the buffer is on the first device
     hipEvent_t copy_begin = nullptr, copy_end = nullptr;  // timing of the peer copy
@@ -149,6 +151,11 @@ static int frame_create_impl(rt_frame* f, const rt_scene_desc* scene, const rt_c
     f->device0 = devices[0];
     f->stripe = stripe_rows ? stripe_rows : rt_stripe_rows(info->height, f->n);
     f->part.resize(f->n);
+    // RT_DEBUG_FRAME_STAGING=1 (tests): every context but the first is gathered as if it were on
+    // another device, so the staging buffers, the peer copies and their event hand-offs run on a
+    // one-GPU box too (hipMemcpyPeerAsync from a device to itself is a device-to-device copy).
+    const char* fs = std::getenv("RT_DEBUG_FRAME_STAGING");
+    const bool force_staging = fs && std::strcmp(fs, "0") != 0;
     // one KD build for every context (rt_create deep-copies it to each device)
     rt_kd_tree* built = nullptr;
     const rt_kd_tree* tree = tree_in;
@@ -177,6 +184,7 @@ static int frame_create_impl(rt_frame* f, const rt_scene_desc* scene, const rt_c
         p.tiles.resize(nt);
         rt_stripe_tiles(f->width, f->height, f->stripe, k, f->n, p.tiles.data(), nt, &nt);
         for (const rt_tile& t : p.tiles) p.npix += (uint64_t)t.w * t.h;
+        p.remote = p.device != f->device0 || (force_staging && k > 0);
         FCHK(f, hipSetDevice(p.device));
         FCHK(f, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
         FCHK(f, hipEventCreateWithFlags(&p.copied, hipEventDisableTiming));
@@ -203,7 +211,7 @@ static int frame_create_impl(rt_frame* f, const rt_scene_desc* scene, const rt_c
     const uint64_t fpix = (uint64_t)f->width * f->height;
     if (hipMalloc(&f->frame, fpix * 4 * sizeof(float)) != hipSuccess) return ferr(f, RT_ERR_OOM, "frame alloc failed");
     for (Part& p : f->part)
-        if (p.device != f->device0 && p.npix && hipMalloc(&p.staging, p.npix * 4 * sizeof(float)) != hipSuccess)
+        if (p.remote && p.npix && hipMalloc(&p.staging, p.npix * 4 * sizeof(float)) != hipSuccess)
             return ferr(f, RT_ERR_OOM, "staging alloc failed");
     return RT_OK;
 }
@@ -245,7 +253,7 @@ extern "C" int rt_frame_render(rt_frame* f, uint64_t sample_begin, uint32_t samp
         FCHK(f, hipSetDevice(p.device));
         // the last gather placed (or copied) this buffer before the new fold may write it: the
         // context's folds wait for what its caller stream holds at the call
-        if (f->gathered) FCHK(f, hipStreamWaitEvent(p.stream, p.device == f->device0 ? f->placed : p.copied, 0));
+        if (f->gathered) FCHK(f, hipStreamWaitEvent(p.stream, p.remote ? p.copied : f->placed, 0));
         const int st = rt_render_device_async(p.ctx, p.tiles.data(), (uint32_t)p.tiles.size(), sample_begin,
                                               sample_count, p.buf, p.stream);
         if (st) return ferr(f, st, "context " + std::to_string(k) + ": " + rt_last_error(p.ctx));
@@ -257,7 +265,7 @@ extern "C" int rt_frame_render(rt_frame* f, uint64_t sample_begin, uint32_t samp
 // stripes into the frame, and (out_host) the read-back.  Ordered after every enqueued render.
 static int gather_enqueue(rt_frame* f, float* out_host, float* out_dev) {
     for (Part& p : f->part) {
-        if (!p.npix || p.device == f->device0) continue;
+        if (!p.npix || !p.remote) continue;
         FCHK(f, hipSetDevice(p.device));
         // a staging buffer the previous placement may still read
         if (f->gathered) FCHK(f, hipStreamWaitEvent(p.stream, f->placed, 0));
@@ -269,7 +277,7 @@ static int gather_enqueue(rt_frame* f, float* out_host, float* out_dev) {
     for (Part& p : f->part) {
         if (!p.npix) continue;
         FCHK(f, hipSetDevice(p.device));
-        FCHK(f, hipEventRecord(p.copied, p.stream));  // same-device contexts: the render is done
+        FCHK(f, hipEventRecord(p.copied, p.stream));  // local contexts: the render is done
     }
     FCHK(f, hipSetDevice(f->device0));
     for (Part& p : f->part)
@@ -344,7 +352,7 @@ extern "C" int rt_frame_get_stats(rt_frame* f, rt_frame_stats* out) {
     for (Part& p : f->part) {
         float ms = 0.f;
         if (p.ctx && rt_last_kernel_ms(p.ctx, &ms) == RT_OK) out->render_ms_max = std::max(out->render_ms_max, ms);
-        if (f->gathered && p.npix && p.device != f->device0) {
+        if (f->gathered && p.npix && p.remote) {
             FCHK(f, hipSetDevice(p.device));
             FCHK(f, hipEventElapsedTime(&ms, p.copy_begin, p.copy_end));
             out->peer_copy_ms_max = std::max(out->peer_copy_ms_max, ms);

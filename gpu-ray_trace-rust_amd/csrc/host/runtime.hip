@@ -24,6 +24,7 @@
 #include "../kernel/device_scene.h"
 #include "host_internal.h"
 #include "mesh_flatten.h"
+#include "treelet.h"
 
 using namespace rtd;
 using namespace rth;
@@ -31,7 +32,7 @@ using namespace rth;
 // Radiance buffer cap per queue launch (floats): 16 GiB of 288 GB HBM, so a 1000-spp step of a
 // 1200x600 frame (8.6 GB) is one launch.  Every launch ends in a drain tail (lanes idle while the
 // last paths finish): walled's bench step ran 3.4% faster as one launch than as three of 334 spp
-// (4 GiB cap).  RT_DEBUG_RADIANCE_GIB overrides it; only what a launch needs is allocated.
+// (4 GiB cap).  RT_DEBUG_LAUNCH radiance_gib overrides it; only what a launch needs is allocated.
 static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 
 // Overlapped queue launches rotate over pipeline slots, each with its own stream, radiance
@@ -54,8 +55,8 @@ static constexpr uint64_t QUEUE_RADIANCE_FLOATS = 1ull << 32;
 // 356; 8 slots, 1/4 grid 370 (1/6: 350, 1/8: 318); 12 slots, 1/6 389, 1/8 400, 1/10 380;
 // biplane / spaceship launches (2 slots) lose with a smaller grid (1/2: -14% / -2%), so they keep
 // the full one.  The first launch of an idle pipeline (and every synchronous call) keeps the full
-// grid too.  RT_DEBUG_PIPELINE_SLOTS (2-32) and RT_DEBUG_GRID_DIV (1-64) override.
-constexpr int N_SLOTS = 32;          // slots a context holds (RT_DEBUG_PIPELINE_SLOTS up to this)
+// grid too.  RT_DEBUG_LAUNCH slots (2-32) and grid_div (1-64) override.
+constexpr int N_SLOTS = 32;          // slots a context holds (RT_DEBUG_LAUNCH slots up to this)
 // A launch's item counters: one 128-B line per shard of its items (trace.hip RT_QSHARDS, <= 32)
 constexpr size_t QUEUE_BYTES = 32 * 128;
 static uint32_t slots_for_queues(int hw_queues) {
@@ -109,7 +110,6 @@ struct rt_ctx {
     uint32_t* d_pixmap = nullptr;     // launch pixel -> (y << 16 | x), multi-tile launches
     uint4* d_pixq = nullptr;          // queue order of the launch pixels (LaunchArgs::pix_q)
     uint32_t pix_block = 1;           // RT_DEBUG_PIX_BLOCK: the queue order's blocks are pix_block x pix_block
-    uint32_t pix_order = 0;           // RT_DEBUG_PIX_ORDER (experiment): 0 raster, 1 reverse, 2 centre first, 3 Morton
     uint64_t d_pixmap_cap = 0;
     std::vector<DevTile> pixmap_tiles;  // the tiles d_pixmap was built for
     float4* d_out = nullptr;
@@ -117,19 +117,19 @@ struct rt_ctx {
     DevCounts* d_counts = nullptr;
     uint64_t lane_capacity = 0;   // lanes resident at the kernel's occupancy
     uint32_t n_cu = 0;
-    uint32_t forced_k = 0;        // RT_DEBUG_LANES_PER_PIXEL (tests / tuning)
+    uint32_t forced_k = 0;        // RT_DEBUG_SCHED=direct:K (tests / tuning)
     int sched = 0;                // RT_DEBUG_SCHED: 0 auto, 1 direct, 2 queue
-    uint64_t queue_floats = 0;    // RT_DEBUG_RADIANCE_GIB: radiance buffer cap per queue launch
-    bool overlap = true;          // RT_DEBUG_PIPELINE: launch i + 1 may start during launch i's drain
+    uint64_t queue_floats = 0;    // radiance buffer cap per queue launch (RT_DEBUG_LAUNCH radiance_gib / radiance_floats)
+    bool overlap = true;          // launch i + 1 may start during launch i's drain (RT_DEBUG_LAUNCH overlap)
     uint64_t overlap_max_items = 1ull << 27;  // ... when it has at most this many samples
-    uint32_t n_slots = 0;         // RT_DEBUG_PIPELINE_SLOTS: slots the overlapped launches rotate over (0: by size)
+    uint32_t n_slots = 0;         // RT_DEBUG_LAUNCH slots: slots the overlapped launches rotate over (0: by size)
     uint32_t small_slots = 8;     // slots of small overlapped launches (slots_for_queues)
     uint32_t mid_slots = 2;       // slots of larger overlapped launches (mid_slots_for)
     uint32_t small_div = 0;       // grid share of a small launch behind a busy pipeline (0: small_grid_div)
-    uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_DEBUG_SMALL_LAUNCH_ITEMS: launches this size or less are small
-    uint32_t grid_div = 0;        // RT_DEBUG_GRID_DIV; 0: small_grid_div(the launch's slots)
-    uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_DEBUG_QUEUE_SHARDS)
-    uint64_t group_items = 0;     // rt_render_to_target: samples per batch group (RT_DEBUG_GROUP_ITEMS; 0: GROUP_ITEMS)
+    uint64_t small_items = SMALL_LAUNCH_ITEMS;  // RT_DEBUG_LAUNCH small_items: launches this size or less are small
+    uint32_t grid_div = 0;        // RT_DEBUG_LAUNCH grid_div; 0: small_grid_div(the launch's slots)
+    uint32_t queue_shards = 1;    // item counters per queue launch (queue_shards; RT_DEBUG_LAUNCH shards)
+    uint64_t group_items = 0;     // rt_render_to_target: samples per batch group (RT_DEBUG_LAUNCH group_items; 0: GROUP_ITEMS)
     float last_ms = 0.f;
     std::string err;
 };
@@ -286,20 +286,20 @@ static bool pack_texels_u8(const rt_scene_desc* scene, const std::vector<DevTex>
 // Item counters of a queue launch (trace.hip qgrab).  Each grab is one device-scope atomic; on a
 // single counter they serialise once items are cheap: triangles.yml (6 primitives, kd depth 0,
 // ~24 us per item and lane) at 10 spp made 112 K of them per 1.4 ms launch, and 8 counters (one
-// shard of the items per XCD) ran it 4,937 -> 14,120 Msamples/s.  Large scenes lose with shards
-// (spaceship_r1 4096^2 -5.4%, biplane -8%, walled -0.6%: one counter keeps the whole chip on
-// one window of consecutive items), so only scenes of at most 64 primitives with triangles are
-// sharded (the sphere-only kernel's grabs are already 256 items: RT_QMIN_SPH).
-static uint32_t queue_shards(uint32_t n_spheres, uint32_t n_free_tris, size_t n_mesh_tris) {
-    const uint64_t n = (uint64_t)n_spheres + n_free_tris + n_mesh_tris;
-    if ((n_free_tris + n_mesh_tris) > 0 && n <= 64) return 8u;
-    // Scenes too large for one XCD's 4 MB L2 (a380: 127 K triangles, ~10 MB of nodes and
-    // primitives): each XCD walks its own shard of the launch's items (a wave starts on shard
-    // blockIdx % 8, and workgroups are dealt to the XCDs round-robin), so its waves are on a
-    // window of pixels of their own and its L2 holds a smaller window's geometry.  a380 +1.6% in the bench's config shape, +4..11% in
-    // synchronous launches; biplane and spaceship keep one counter (shards cost them 3%).
-    if (n >= (1u << 16)) return 8u;
-    return 1u;
+// shard of the items per XCD) ran it 4,937 -> 14,120 Msamples/s.  So a tiny scene (tiny_scene:
+// at most 64 primitives, with triangles) gets 8 shards.  So does a scene whose traversal data
+// (nodes, refs and leaf-test primitives) exceeds one XCD's 4 MiB L2: each XCD then walks its own
+// shard of the launch's items (a wave starts on shard blockIdx % 8, and workgroups are dealt to
+// the XCDs round-robin), so at any moment its waves are on a window of pixels of their own and its
+// L2 holds a smaller window's geometry.  Measured points: a380 (~10 MiB) +4..11% in
+// synchronous launches, L2 hit rate 0.935 -> 0.944; spaceship_r1 and biplane (well under 4 MiB)
+// lose 3% with shards and keep one counter.  Scenes between those sizes are unmeasured.
+constexpr uint64_t XCD_L2_BYTES = 4ull << 20;
+static bool tiny_scene(uint32_t n_spheres, uint32_t n_free_tris, size_t n_mesh_tris) {
+    return (n_free_tris + n_mesh_tris) > 0 && (uint64_t)n_spheres + n_free_tris + n_mesh_tris <= 64;
+}
+static uint32_t queue_shards(bool tiny, uint64_t traversal_bytes) {
+    return (tiny || traversal_bytes > XCD_L2_BYTES) ? 8u : 1u;
 }
 
 // A pipeline slot's stream, fold event and item counter, created on the slot's first use: HIP
@@ -467,6 +467,14 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         n.x |= lead << LEAF_LEAD_SHIFT;
     }
 
+    // The cooperative descent's treelets (treelet.h): the same tree, three levels per record.
+    std::vector<uint32_t> tl_words, tl_leaves;
+    {
+        std::vector<uint32_t> flat(2 * nodes.size());
+        for (size_t i = 0; i < nodes.size(); ++i) flat[2 * i] = nodes[i].x, flat[2 * i + 1] = nodes[i].y;
+        if (!build_treelets(flat, &tl_words, &tl_leaves)) return set_err(c, RT_ERR_UNSUPPORTED, "KD tree too large for treelets");
+    }
+
     // Direct-light sampling (radiance.rs:89-120): every AABB'd renderable as a device ref in
     // renderable order (the shadow ray's brute-force closest_ray_hit), and the emissive spheres
     // with their position in that list.  Cube maps hit at +inf and can never be a shadow ray's
@@ -485,6 +493,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         }
     }
 
+    bool tiny = false;  // tiny_scene (set with the leaf-test pool below)
     std::vector<float4> sph(scene->n_spheres);
     std::vector<DevMat> sph_mat(scene->n_spheres);
     for (uint32_t i = 0; i < scene->n_spheres; ++i) {
@@ -565,18 +574,29 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.n_emit = (uint32_t)emit.size();
     d.dls = emit.empty() ? 0u : 1u;  // no emitter: the DLS term is exactly zero
     if ((st = upload(c, refs, &d.refs))) return st;
+    {
+        std::vector<uint4> tl4(tl_words.size() / 4);
+        std::memcpy(tl4.data(), tl_words.data(), tl_words.size() * sizeof(uint32_t));
+        std::vector<uint2> tlf(tl_leaves.size() / 2);
+        std::memcpy(tlf.data(), tl_leaves.data(), tl_leaves.size() * sizeof(uint32_t));
+        if ((st = upload(c, tl4, &d.tl))) return st;
+        if ((st = upload(c, tlf, &d.tleaf))) return st;
+    }
     if ((st = upload(c, sph, &d.sph))) return st;
     if ((st = upload(c, sph_mat, &d.sph_mat))) return st;
     {   // the leaf-test pool: spheres, free triangles, mesh triangles, 3 float4 each
         const size_t n_mesh = mf.tris.size();
         if ((uint64_t)scene->n_spheres + scene->n_free_tris + n_mesh >= (1ull << 30))
             return set_err(c, RT_ERR_INVALID_ARG, "too many primitives");
-        c->queue_shards = queue_shards(scene->n_spheres, scene->n_free_tris, n_mesh);
-        // A scene that small (triangles.yml: 6 primitives, ~24 us per item and lane) makes even a
-        // 7.2 M-sample launch mostly start-up and drain: its launches up to 2^24 samples go to the
+        tiny = tiny_scene(scene->n_spheres, scene->n_free_tris, n_mesh);
+        const uint64_t trav_bytes = nodes.size() * sizeof(uint2) + refs.size() * sizeof(uint32_t) +
+                                    3 * sizeof(float4) * ((uint64_t)scene->n_spheres + scene->n_free_tris + n_mesh);
+        c->queue_shards = queue_shards(tiny, trav_bytes);
+        // A tiny scene (triangles.yml: 6 primitives, ~24 us per item and lane) makes even a 7.2
+        // M-sample launch mostly start-up and drain: its launches up to 2^24 samples go to the
         // small-launch pipeline (round 3, tools/gpu_a380_calib.py, 10 spp per launch: 16,600
         // Msamples/s on 2 slots with the full grid, 17,700-18,300 on 4-12 slots with a share).
-        if (c->queue_shards > 1) c->small_items = 1ull << 24;
+        if (tiny) c->small_items = 1ull << 24;
         std::vector<float4> pool(3 * ((size_t)scene->n_spheres + scene->n_free_tris + n_mesh), make_float4(0.f, 0.f, 0.f, 0.f));
         for (uint32_t i = 0; i < scene->n_spheres; ++i) pool[3 * (size_t)i] = sph[i];
         std::memcpy(pool.data() + 3 * (size_t)scene->n_spheres, ftri.data(), ftri.size() * sizeof(float4));
@@ -698,99 +718,94 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     c->lane_capacity = (uint64_t)prop.multiProcessorCount * 4 /*SIMD*/ * 7 /*waves*/ * 64;
     pc.mark("accum_props");
     c->n_cu = (uint32_t)prop.multiProcessorCount;
+    // RT_DEBUG_SCHED=direct[:K]: the direct schedule (K lanes per pixel, 1/2/4/8; the default K
+    // follows the launch's pixels), the tests' second path; "queue" is the default.
     if (const char* e = debug_env("SCHED")) {
-        if (!std::strcmp(e, "direct")) c->sched = 1;
-        else if (!std::strcmp(e, "queue")) c->sched = 2;
-    }
-    if (const char* e = debug_env("LANES_PER_PIXEL")) {
-        unsigned long v = std::strtoul(e, nullptr, 10);
-        if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
-    }
-    c->queue_floats = QUEUE_RADIANCE_FLOATS;
-    if (const char* e = debug_env("RADIANCE_GIB")) {
-        unsigned long v = std::strtoul(e, nullptr, 10);
-        if (v >= 1 && v <= 64) c->queue_floats = (uint64_t)v << 28;
+        if (!std::strncmp(e, "direct", 6)) {
+            c->sched = 1;
+            if (e[6] == ':') {
+                const unsigned long v = std::strtoul(e + 7, nullptr, 10);
+                if (v == 1 || v == 2 || v == 4 || v == 8) c->forced_k = (uint32_t)v;
+            }
+        } else if (!std::strcmp(e, "queue")) {
+            c->sched = 2;
+        }
     }
     // Traversal of the queue kernels: the reference's stack (kdtree.rs:66-104) or stackless
     // kd-restart with push-down, bit-identical (trace.hip stack_search_coop).  The stack is faster
-    // on the mesh scenes (DESIGN.md §8); the sphere-only kernel, which descends for 0.05 nodes
+    // on the mesh scenes (DESIGN.md §5); the sphere-only kernel, which descends for 0.05 nodes
     // per sample, runs stackless and needs no global stack.  RT_DEBUG_KD_RESTART=0/1 overrides.
-    // RT_DEBUG_KD_RESTART=2: stackless with the wave's leaf triangles staged in LDS per round (the
-    // general kernel; measured slower).
     // Camera-ray packets in the general queue kernel (trace.hip closest_packet), bit-identical to
     // the cooperative search; RT_DEBUG_PACKET=0 turns them off.  RT_DEBUG_PIX_BLOCK=1 gives the queue the
     // launch pixels in row order instead of 8 x 8 blocks (the same images).
     d.packet = 1u;
     if (const char* e = debug_env("PACKET")) d.packet = std::strcmp(e, "0") ? 1u : 0u;
     c->pix_block = RT_PIX_BLOCK;
-    if (const char* e = debug_env("PIX_ORDER")) c->pix_order = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = debug_env("PIX_BLOCK")) {
         const unsigned long v = std::strtoul(e, nullptr, 10);
         if (v >= 1 && v <= 64) c->pix_block = (uint32_t)v;
     }
     d.restart = d.spheres_only ? 1u : 0u;
-    if (const char* e = debug_env("KD_RESTART")) {
-        const unsigned long v = std::strtoul(e, nullptr, 10);
-        d.restart = v > 2 ? 1u : (uint32_t)v;
-    }
-    // The pool kernel (trace.hip g_pool4): the general kernel with every leaf-testable primitive
-    // resident in LDS, stackless.  RT_DEBUG_POOL: 0 off, 768 / 1024 that many threads per workgroup
-    // (when the pool fits), "auto" 768 when keys + pool fit in half a CU's LDS (two workgroups per
-    // CU), else 1024 when they fit in the whole.
-    d.n_pool = scene->n_spheres + scene->n_free_tris + (uint32_t)mf.tris.size();
-    d.pool_nt = 0;
-    if (!d.spheres_only && !d.dls) {
-        const char* e = debug_env("POOL");
-        const std::string mode = e ? e : "0";
-        constexpr size_t LDS_CU = 160u * 1024u;
-        auto fits = [&](uint32_t nt, size_t budget) { return pool_lds_bytes(nt, d.n_pool) <= budget; };
-        if (mode == "auto") d.pool_nt = fits(768, LDS_CU / 2) ? 768u : (fits(1024, LDS_CU) ? 1024u : 0u);
-        else if (mode == "768" && fits(768, LDS_CU)) d.pool_nt = 768;
-        else if (mode == "1024" && fits(1024, LDS_CU)) d.pool_nt = 1024;
-        if (d.pool_nt) d.restart = 1;  // the pool kernel is stackless (its LDS holds no stack)
-    }
+    if (const char* e = debug_env("KD_RESTART")) d.restart = std::strcmp(e, "0") ? 1u : 0u;
+    // The cooperative descent over treelets (trace.hip stack_search_coop TL), RT_DEBUG_TREELET=1;
+    // the default descends over the nodes, a child pair per level (treelets measured 19-27%
+    // slower).
+    d.treelet = 0u;
+    if (const char* e = debug_env("TREELET")) d.treelet = d.tl && std::strcmp(e, "0") ? 1u : 0u;
     // Overlapped launches pay off while a launch's drain tail is a sizeable share of it: mesh
-    // launches (8-10 ms tails, DESIGN.md §8) and small sphere-only ones — walled's ~0.4 ms tail on
+    // launches (8-10 ms tails, DESIGN.md §5) and small sphere-only ones — walled's ~0.4 ms tail on
     // one rank's 90 M-sample share at N = 8 (9 ms): +3% overlapped, while at 180 M it is neutral
     // and at 360 / 720 M a fold beside the next trace grid costs 1%.  enqueue_queue overlaps
-    // launches of at most overlap_max_items (2^27) samples.  RT_DEBUG_PIPELINE=0/1/2 overrides.
+    // launches of at most overlap_max_items (2^27) samples.
     c->overlap = true;
-    if (const char* e = debug_env("PIPELINE_SLOTS")) {
-        const unsigned long v = std::strtoul(e, nullptr, 10);
-        if (v >= 2 && v <= (unsigned long)N_SLOTS) c->n_slots = (uint32_t)v;
-    }
+    c->queue_floats = QUEUE_RADIANCE_FLOATS;
     {
         const char* q = std::getenv("GPU_MAX_HW_QUEUES");  // what HIP read when it started
         const int hwq = q && std::atoi(q) > 0 ? std::atoi(q) : 4;
         c->small_slots = slots_for_queues(hwq);
         c->mid_slots = mid_slots_for(c->small_slots);
-        // A tiny scene (queue_shards > 1, items of ~24 us) runs its launches of up to 2^24 samples
-        // on the small-launch pipeline (above), with the mid-size slot count and half the grid each
+        // A tiny scene (items of ~24 us) runs its launches of up to 2^24 samples on the
+        // small-launch pipeline (above), with the mid-size slot count and half the grid each
         // (round 4, triangles.yml's 7.2 M-sample launches at 16 queues: 12 slots with an eighth of
         // the grid 16,000 Msamples/s, 4 / 6 slots with a half 17,100 / 17,000, 2 slots with the full
         // grid 16,700).
-        if (c->queue_shards > 1) {
+        if (tiny) {
             c->small_slots = c->mid_slots;
             if (c->small_slots >= 4) c->small_div = 2;
         }
     }
-    if (const char* e = debug_env("QUEUE_SHARDS")) {
-        const unsigned long v = std::strtoul(e, nullptr, 10);
-        if (v >= 1 && v <= 32) c->queue_shards = (uint32_t)v;
-    }
-    if (const char* e = debug_env("SMALL_LAUNCH_ITEMS")) c->small_items = std::strtoull(e, nullptr, 10);
-    if (const char* e = debug_env("GROUP_ITEMS")) c->group_items = std::strtoull(e, nullptr, 10);
-    if (const char* e = debug_env("GRID_DIV")) {
-        const unsigned long v = std::strtoul(e, nullptr, 10);
-        if (v >= 1 && v <= 64) c->grid_div = (uint32_t)v;
-    }
-    if (const char* e = debug_env("PIPELINE")) {  // 0: never, 1: below the item limit, 2: always
-        c->overlap = std::strcmp(e, "0") != 0;
-        if (!std::strcmp(e, "2")) c->overlap_max_items = ~0ull;
-    }
-    if (const char* e = debug_env("RADIANCE_FLOATS")) {  // tests: force split launches
-        unsigned long long v = std::strtoull(e, nullptr, 10);
-        if (v >= 3 && v <= (1ull << 34)) c->queue_floats = (uint64_t)v;
+    // RT_DEBUG_LAUNCH="key=value,...": the launch pipeline's A/B and test settings (INTEGRATION.md
+    // §6): overlap=0|1|2 (never / up to overlap_max_items / always), slots=2..32, grid_div=1..64,
+    // small_items=N, group_items=N, shards=1..32, radiance_gib=1..64, radiance_floats=N (tests:
+    // force split launches).  Unknown keys are ignored.
+    if (const char* e = debug_env("LAUNCH")) {
+        for (const char* k = e; *k;) {
+            const char* eq = std::strchr(k, '=');
+            if (!eq) break;
+            const std::string key(k, (size_t)(eq - k));
+            char* endp = nullptr;
+            const unsigned long long v = std::strtoull(eq + 1, &endp, 10);
+            if (key == "overlap") {
+                c->overlap = v != 0;
+                if (v == 2) c->overlap_max_items = ~0ull;
+            } else if (key == "slots" && v >= 2 && v <= (unsigned long long)N_SLOTS) {
+                c->n_slots = (uint32_t)v;
+            } else if (key == "grid_div" && v >= 1 && v <= 64) {
+                c->grid_div = (uint32_t)v;
+            } else if (key == "small_items") {
+                c->small_items = v;
+            } else if (key == "group_items") {
+                c->group_items = v;
+            } else if (key == "shards" && v >= 1 && v <= 32) {
+                c->queue_shards = (uint32_t)v;
+            } else if (key == "radiance_gib" && v >= 1 && v <= 64) {
+                c->queue_floats = (uint64_t)v << 28;
+            } else if (key == "radiance_floats" && v >= 3 && v <= (1ull << 34)) {
+                c->queue_floats = (uint64_t)v;
+            }
+            if (*endp != ',') break;
+            k = endp + 1;
+        }
     }
     return RT_OK;
 }
@@ -928,38 +943,6 @@ static int prepare_tiles(rt_ctx* c, const rt_tile* tiles, uint32_t n_tiles, uint
                                 const uint64_t key = rt_rng_pixel_key(c->sc.seed, fy * c->sc.width + fx);
                                 pq.push_back(make_uint4(pm[o], o, (uint32_t)key, (uint32_t)(key >> 32)));
                             }
-            if (c->pix_order && B > 1) {  // experiment: the same blocks in another order
-                const size_t bs = (size_t)B * B;
-                std::vector<std::pair<double, size_t>> key;  // (sort key, first entry of the block)
-                for (size_t b0 = 0; b0 < pq.size();) {
-                    const uint32_t xy = pq[b0].x;
-                    size_t b1 = b0 + 1;  // a block's entries share (x / B, y / B) and its tile
-                    while (b1 < pq.size() && b1 - b0 < bs && (pq[b1].x & 0xffffu) / B == (xy & 0xffffu) / B &&
-                           (pq[b1].x >> 16) / B == (xy >> 16) / B)
-                        ++b1;
-                    const double dx = (double)(xy & 0xffffu) - 0.5 * c->sc.width, dy = (double)(xy >> 16) - 0.5 * c->sc.height;
-                    double k = c->pix_order == 1 ? -(double)b0 : dx * dx + dy * dy;
-                    if (c->pix_order == 3) {  // Morton order of the blocks: a compact 2-D window in flight
-                        uint64_t m = 0;
-                        const uint32_t bx = (xy & 0xffffu) / B, by = (xy >> 16) / B;
-                        for (int bit = 0; bit < 16; ++bit)
-                            m |= (uint64_t)((bx >> bit) & 1u) << (2 * bit) | (uint64_t)((by >> bit) & 1u) << (2 * bit + 1);
-                        k = (double)m;
-                    }
-                    key.push_back({k, b0});
-                    b0 = b1;
-                }
-                std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-                std::vector<uint4> re;
-                re.reserve(pq.size());
-                for (const auto& k : key) {
-                    const uint32_t xy = pq[k.second].x;
-                    for (size_t i = k.second; i < pq.size() && i - k.second < bs && (pq[i].x & 0xffffu) / B == (xy & 0xffffu) / B &&
-                                              (pq[i].x >> 16) / B == (xy >> 16) / B; ++i)
-                        re.push_back(pq[i]);
-                }
-                pq.swap(re);
-            }
             if (pix > c->d_pixmap_cap) {
                 if (c->d_pixmap) (void)hipFree(c->d_pixmap);
                 if (c->d_pixq) (void)hipFree(c->d_pixq);
@@ -1022,8 +1005,8 @@ static int ensure_radiance(rt_ctx* c, Slot& sl, uint64_t floats) {
 static constexpr uint32_t SAMPLES_PER_LANE_CHUNK = 64;
 
 // Schedule: the queue (persistent lanes over (pixel, sample) items, tools/variant_bench.py:
-// walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_DEBUG_SCHED=direct or
-// RT_DEBUG_LANES_PER_PIXEL asks for the direct one-lane-per-pixel schedule (kept for A/B and as the
+// walled 3040 -> 3625, biplane 17 -> 65-70 Msamples/s) unless RT_DEBUG_SCHED=direct[:K]
+// asks for the direct one-lane-per-pixel schedule (kept for A/B and as the
 // tests' second path).
 static bool use_queue(const rt_ctx* c) {
     if (c->forced_k) return false;
@@ -1096,7 +1079,7 @@ static int enqueue_queue(rt_ctx* c, LaunchArgs a, uint64_t n_out, uint64_t sampl
         }
         const uint32_t n_slots = c->n_slots ? c->n_slots
                                             : (small ? c->small_slots : (a.n_items <= MID_LAUNCH_ITEMS ? c->mid_slots : 2u));
-        // the grid share follows the slots this launch rotates over (RT_DEBUG_GRID_DIV overrides)
+        // the grid share follows the slots this launch rotates over (RT_DEBUG_LAUNCH grid_div overrides)
         const uint32_t grid_div = c->grid_div ? c->grid_div : (c->small_div ? c->small_div : small_grid_div(n_slots));
         if (overlap) c->cur_slot = (c->cur_slot + 1) % n_slots;
         for (uint32_t k = 0; k < (overlap ? n_slots : 1u); ++k) {

@@ -73,12 +73,15 @@ struct DevScene {
     uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
     uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
     uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
-    uint32_t restart;       // queue kernels: 0 stack, 1 stackless (kd-restart with push-down), 2 stackless + LDS triangle slabs
+    uint32_t restart;       // queue kernels: 0 stack, 1 stackless (kd-restart with push-down)
     uint32_t packet;        // general queue kernel: camera rays may be traced as packets (closest_packet)
-    // The pool kernel (trace.hip g_pool4): every leaf-testable primitive resident in LDS for the
-    // launch; pool_nt = its threads per workgroup (768 / 1024), 0 = off; n_pool = primitives.
-    uint32_t pool_nt;
-    uint32_t n_pool;
+    // The same tree as 3-level treelets (host/treelet.h): 64-B records (tl, 4 x uint4 each, the
+    // first three loaded) and the leaves reached from them (tleaf, the node layout), read by the
+    // cooperative descent when `treelet` is set; a stack entry or restart point is a treelet
+    // index << 3 | position.
+    const uint4* tl;
+    const uint2* tleaf;
+    uint32_t treelet;
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r
@@ -186,6 +189,5 @@ hipError_t launch_trace_queue(const LaunchArgs& a, uint32_t n_blocks, hipStream_
 hipError_t queue_blocks_per_cu(const LaunchArgs& a, int* blocks);
 size_t queue_gstack_bytes(const LaunchArgs& a, uint32_t n_blocks);  // 0: the stack is in LDS
 uint32_t queue_block_threads(const LaunchArgs& a);  // threads per workgroup of the scene's queue kernel
-size_t pool_lds_bytes(uint32_t pool_nt, uint32_t n_pool);  // dynamic LDS of the pool kernel
 
 }  // namespace rtd

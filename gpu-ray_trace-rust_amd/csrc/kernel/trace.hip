@@ -45,7 +45,6 @@ constexpr int RT_REGEN_MIN_BATCH = 1;  // the sphere-only kernel with batched st
 constexpr int RT_REGEN_MIN_GEN = 16;  // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
 constexpr int RT_MIN_WAVES = 7;  // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
 constexpr int RT_MIN_WAVES_GEN = 8;  // general (triangle / mesh) kernels: 8 -> <=64 VGPRs; latency-bound, +2..7% over 7 (spills outside the pass loop)
-constexpr int RT_SLAB_TRIS = 96;  // stackless general kernel: primitives per wave staged in LDS per round (0: none)
 constexpr int RT_OWNER_LOOP = 8;  // cooperative pass: owners of a pass found by a readlane loop when at most this many leaves end in it (0: binary search)
 constexpr int RT_PAIR_FETCH = 1;  // cooperative descent: a node's two children loaded together, before its decision (a380 +3%, biplane +3%)
 constexpr int RT_PIX_KEY = 1;  // queue kernels: the pixel's stream key from the queue-order table (one SplitMix64 round per path start, not two)
@@ -700,49 +699,6 @@ struct PkScene {
 // win (see leaf_closest).  The owner then re-tests the winning ref for its barycentrics.
 __shared__ unsigned long long g_coop_key[BLOCK];
 
-// Whole-pool residency (the pool kernel, DevScene::pool_nt > 0).  A scene whose leaf-testable
-// primitives fit in LDS keeps all of them there for the whole launch, copied once per workgroup
-// at its start, so a cooperative pass reads a pair's primitive with ds_read instead of three 16-B
-// gathers through the vector-memory return path (TA / TD), which bounds the mesh kernels
-// (spaceship_r1: 44.5 of its 78.3 vector wave-loads per sample were those gathers).  Unlike the
-// per-round slabs of RT_DEBUG_KD_RESTART=2 nothing is copied again during the launch.  The pool
-// kernel's dynamic LDS: the workgroup's leaf-minimum keys (PNT x 8 B, coop_leaf's g_coop_key),
-// then the pool as three arrays, 36 B per primitive, the prim4 values without their padding:
-// A = {v0.xyz, e1.x}, B = {e1.yz, e2.xy}, C = e2.z; a sphere is A = {c, r}, B = C = 0.  PNT =
-// threads per workgroup: 768 (two workgroups per CU, 6 waves per SIMD, when keys and pool fit in
-// half the CU's 160 KiB) or 1024 (one per CU, 4 waves per SIMD).
-extern __shared__ float4 g_pool4[];
-template <int PNT>
-__device__ __forceinline__ unsigned long long* coop_keys() {
-    if constexpr (PNT > 0) return reinterpret_cast<unsigned long long*>(g_pool4);
-    else return g_coop_key;
-}
-template <int PNT>
-__device__ __forceinline__ void pool_load(uint32_t n, uint32_t i, float4& a0, float4& a1, float4& a2) {
-    const float4* A = g_pool4 + PNT / 2;
-    const float4 x = A[i], y = A[n + i];
-    const float z = reinterpret_cast<const float*>(A + 2 * (size_t)n)[i];
-    a0 = x;
-    a1 = make_float4(x.w, y.x, y.y, 0.f);
-    a2 = make_float4(y.z, y.w, z, 0.f);
-}
-template <int PNT>
-__device__ __forceinline__ float4 pool_sphere(uint32_t i) { return (g_pool4 + PNT / 2)[i]; }
-// The whole workgroup copies the pool from prim4 (sc.n_pool primitives); a __syncthreads follows.
-template <int PNT>
-__device__ __forceinline__ void pool_fill(const DevScene& sc) {
-    float4* A = g_pool4 + PNT / 2;
-    float* C = reinterpret_cast<float*>(A + 2 * (size_t)sc.n_pool);
-    for (uint32_t i = threadIdx.x; i < sc.n_pool; i += PNT) {
-        const float4* p = sc.prim4 + 3 * (size_t)i;
-        const float4 p0 = p[0], p1 = p[1], p2 = p[2];
-        const bool sph = i < sc.pool_ftri;  // spheres lead the pool
-        A[i] = make_float4(p0.x, p0.y, p0.z, sph ? p0.w : p1.x);
-        A[sc.n_pool + i] = sph ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(p1.y, p1.z, p2.x, p2.y);
-        C[i] = sph ? 0.f : p2.z;
-    }
-}
-
 // Inclusive prefix maximum over the 64 lanes (the DPP pattern of wave_incl_scan with max).
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
@@ -800,69 +756,17 @@ __device__ __forceinline__ uint32_t pass_owner(uint32_t incl, uint32_t total, ui
     return list_owner(incl, w);
 }
 
-// Triangle slabs staged in LDS (the stackless general kernel, whose LDS holds no stack): per
-// round, the distinct leaves of the wave's lanes are copied once into the wave's slab (up to
-// RT_SLAB_TRIS primitives; leaves beyond it keep the global path), as {p0, p1 | ref, p2} with
-// p = the primitive's three pool float4 (DevScene::prim4) and the ref in p1.w.  Rays of one wave
-// start on neighbouring pixels, so most lanes share their leaf: a pair then reads its primitive
-// from LDS instead of a ref and three gathers from L1 / L2 per (ray, primitive) pair.
-__shared__ float4 g_slab[BLOCK / 64][RT_SLAB_TRIS > 0 ? 3 * RT_SLAB_TRIS : 1];
-constexpr uint32_t SLAB_NONE = 0x80000000u;  // a lane's slab delta when its leaf is not staged
-
 // Every lane of the wave must call this (all active); lanes without a leaf pass cnt = 0.
 // Returns the lane's leaf minimum as (bits(l) << 32 | index into sc.refs), ~0 for none; one
 // leaf's refs are contiguous, so the index orders like the position in the leaf.  `key0` is
 // the lane's minimum over refs it tested itself (the leaf's leading spheres).
-template <bool SLAB, int PNT = 0>
 __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, const Ray& r, uint32_t off,
                                                         uint32_t cnt, uint32_t lane, unsigned long long key0) {
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
     const uint32_t wbase = threadIdx.x & ~63u;
-    unsigned long long* const keys = coop_keys<PNT>();
+    unsigned long long* const keys = g_coop_key;
     __hip_atomic_store(&keys[threadIdx.x], key0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    // slab index of item w of this lane's leaf = w + sdelta (SLAB_NONE: not staged); valid
-    // deltas lie in (-2^31, RT_SLAB_TRIS), so the sentinel never collides
-    uint32_t sdelta = SLAB_NONE;
-    if constexpr (SLAB) {
-        float4* slab = g_slab[threadIdx.x >> 6];
-        // lanes grouped by leaf (equal offsets: equal ref lists), groups in lane order of their
-        // first lane, staged while they fit
-        uint64_t pending = __ballot(cnt > 0);
-        uint32_t used = 0, lead_n = 0, sbase = 0;
-        bool staged = false;
-        while (pending) {
-            const uint32_t ld = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
-            const uint32_t o = __builtin_amdgcn_readlane(off, ld), n = __builtin_amdgcn_readlane(cnt, ld);
-            const uint64_t same = __ballot(off == o) & pending;
-            pending &= ~same;
-            if (used + n <= (uint32_t)RT_SLAB_TRIS) {
-                if ((same >> lane) & 1ull) { staged = true; sbase = used; }
-                if (lane == ld) lead_n = n;
-                used += n;
-            }
-        }
-        if (used) {
-            // the staged lists, concatenated, copied by the whole wave (a pass of the same shape
-            // as the test passes below)
-            const uint32_t fincl = wave_incl_scan(lead_n, lane);
-            for (uint32_t fb = 0; fb < used; fb += 64) {
-                const uint32_t w = fb + lane;
-                const uint32_t fo = list_owner(fincl, w);
-                const uint32_t src = w + __shfl(off - (fincl - lead_n), fo);
-                if (w < used) {
-                    const uint32_t ref = sc.refs[src];
-                    const float4* pd = prim_data(sc, ref);
-                    const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
-                    slab[3 * w] = a0;
-                    slab[3 * w + 1] = make_float4(a1.x, a1.y, a1.z, __uint_as_float(ref));
-                    slab[3 * w + 2] = a2;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();  // the slab's writes before any lane's reads
-        }
-        if (staged) sdelta = sbase - (incl - cnt);
-    }
     // item w of a lane's leaf is sc.refs[w + delta]
     const uint32_t delta = off - (incl - cnt);
     for (uint32_t base = 0; base < total; base += 64) {
@@ -873,35 +777,18 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
         Ray ro;
         ro.o = mk(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
         ro.d = mk(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
-        const uint32_t od = SLAB ? __shfl(sdelta, owner) : SLAB_NONE;
         if (w < total) {
-            uint32_t ref;
-            float4 a0, a1, a2;
-            if (SLAB && od != SLAB_NONE) {
-                const float4* sp = g_slab[threadIdx.x >> 6] + 3 * (w + od);
-                a0 = sp[0];
-                a1 = sp[1];
-                a2 = sp[2];
-                ref = __float_as_uint(a1.w);
-            } else {
-                // the primitive's three float4 are loaded before the kind is known (a sphere's
-                // are {c, r} and padding): one round trip to L2 after the ref, not two
-                VC(2, 1);
-                VL(2, sc.refs + idx, 4, true);
-                ref = sc.refs[idx];
-                if constexpr (PNT > 0) {
-                    pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
-                } else {
-                    VC(3, 3);
-                    const float4* pd = prim_data(sc, ref);
-                    VL(3, pd, 16, true);
-                    VL(3, pd + 1, 16, true);
-                    VL(3, pd + 2, 16, true);
-                    a0 = pd[0];
-                    a1 = pd[1];
-                    a2 = pd[2];
-                }
-            }
+            // the primitive's three float4 are loaded before the kind is known (a sphere's are
+            // {c, r} and padding): one round trip to L2 after the ref, not two
+            VC(2, 1);
+            VL(2, sc.refs + idx, 4, true);
+            const uint32_t ref = sc.refs[idx];
+            VC(3, 3);
+            const float4* pd = prim_data(sc, ref);
+            VL(3, pd, 16, true);
+            VL(3, pd + 1, 16, true);
+            VL(3, pd + 2, 16, true);
+            const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
             float l = 0.f, bu, bv;
             bool h;
             if (__builtin_expect((ref >> REF_KIND_SHIFT) == K_SPHERE, 0)) h = sphere_hit(a0, ro, &l);
@@ -910,7 +797,6 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
                 atomicMin(&keys[wbase + owner], ((unsigned long long)__float_as_uint(l) << 32) | idx);
         }
     }
-    if (SLAB) __builtin_amdgcn_wave_barrier();  // every read of this round's slab before the next fill
     return __hip_atomic_load(&keys[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
@@ -926,14 +812,28 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
-template <bool FAST, bool RESTART, bool SLAB, int PNT = 0>
+// Split bits of treelet position p (0..6) from the record's first seven words (treelet.h).
+__device__ __forceinline__ uint32_t sel7(uint4 a, uint4 b, uint32_t p) {
+    const bool b0 = (p & 1u) != 0u, b1 = (p & 2u) != 0u, b2 = (p & 4u) != 0u;
+    const uint32_t x01 = b0 ? a.y : a.x, x23 = b0 ? a.w : a.z, x45 = b0 ? b.y : b.x;
+    const uint32_t lo = b1 ? x23 : x01, hi = b1 ? b.z : x45;
+    return b2 ? hi : lo;
+}
+
+// TL (treelets, DevScene::tl): the descent reads the tree as 3-level treelets (host/treelet.h):
+// one 48-B load brings the splits and axes of a branch and the two levels below it, so a lane
+// decides up to three levels per dependent load instead of one (the node layout's child-pair
+// load per level).  The branches met, their order and their split values are the node tree's:
+// `node` is then a treelet index << 3 | position (stack entries and the restart point too), and
+// the pop resumes at the pushed branch with its far child forced (pop_far).
+template <bool FAST, bool RESTART, bool TL>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
                                                   uint32_t* st) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0, restart = 0;
     int sp = 0;
-    bool done = !active, found = false, pushed = false;
+    bool done = !active, found = false, pushed = false, pop_far = false;
     const uint32_t lane = __lane_id();
     // RT_LEAF_REUSE: the previous leaf's list (its offset in sc.refs: the upload gives identical
     // lists one copy, so equal offsets mean equal lists) and its minimum key
@@ -944,7 +844,9 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     // !RESTART: the pop after a leaf that does not return needs two nodes, the branch it returns to
     // (its b word: children and axis) and the branch below it (the new exit); both are loaded ahead
     // of the leaf's passes, so their trip to L1 / L2 overlaps the passes instead of following them
-    // (A/B at 4-10 spp: a380 and biplane +4..7%, spaceship +-0; the bench configs +-0)
+    // (A/B at 4-10 spp: a380 and biplane +4..7%, spaceship +-0; the bench configs +-0).  TL: the
+    // popped branch's treelet is the next descent's first load, so only the branch below it (its
+    // split word and axis) is loaded ahead.
     uint32_t pop_b = 0;
     uint2 below = make_uint2(0u, 0u);
     auto advance = [&]() -> bool {
@@ -957,8 +859,13 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             --sp;
             // the popped branch's node and the one below it were loaded before the leaf's passes
             float d;
-            (void)split_t<FAST>(make_uint2(0u, pop_b), ax, r, &d);
-            node = (pop_b >> 2) + (d > 0.0f ? 1u : 0u);
+            if (TL) {
+                node = st[sp * BLOCK];
+                pop_far = true;
+            } else {
+                (void)split_t<FAST>(make_uint2(0u, pop_b), ax, r, &d);
+                node = (pop_b >> 2) + (d > 0.0f ? 1u : 0u);
+            }
             entry = top_t;
             if (sp) {
                 top_t = split_t<FAST>(below, ax, r, &d);
@@ -974,10 +881,88 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         unsigned long long key0 = ~0ull;
         VC(12, 1);
         if (!done) {
-            uint2 nd = fetch_node(sc, node);
+            uint2 nd;
+            pushed = false;
+            if constexpr (TL) {
+                // the lane's treelet and position; r0 / r1 / r2 its record's words 0-11
+                uint32_t tn = node >> 3, tp = node & 7u;
+                VC(0, 3);
+                VL(0, sc.tl + 4 * (size_t)tn, 16, true);
+                VL(0, sc.tl + 4 * (size_t)tn + 1, 16, true);
+                VL(0, sc.tl + 4 * (size_t)tn + 2, 16, true);
+                uint4 r0 = sc.tl[4 * (size_t)tn], r1 = sc.tl[4 * (size_t)tn + 1], r2 = sc.tl[4 * (size_t)tn + 2];
+                uint32_t li = 0;
+                // One treelet per iteration: up to three levels decided from the record in
+                // registers (no load between them: positions 0 -> 1..2 -> 3..6 -> an exit), then
+                // one load, the child treelet's record or the leaf's.  Lanes out of phase (one
+                // starting at position 5, another at 0) still share each iteration's single load
+                // latency; a level-per-iteration loop paid one latency per level whenever any lane
+                // of the wave crossed into a new treelet (round 6: -23..-25%, profiles/r6_ab).
+                for (;;) {
+                    bool leaf = false, out = false;
+#pragma unroll
+                    for (int step = 0; step < 3; ++step) {
+                        if (out) continue;
+                        const uint32_t tag = (r1.w >> (2u * tp)) & 3u;
+                        if (tag == RT_KD_LEAF) {  // a leaf inside the treelet
+                            li = r2.y + (uint32_t)__popc(r2.z & ((1u << tp) - 1u));
+                            leaf = out = true;
+                            continue;
+                        }
+                        const uint2 bn = make_uint2(sel7(r0, r1, tp), tag);
+                        float d;
+                        const float t = split_t<FAST>(bn, ax, r, &d);
+                        const bool pos = d > 0.0f;
+                        uint32_t c;
+                        if (!RESTART && pop_far) {  // the popped branch: its far child (kdtree.rs:99-102)
+                            c = pos ? 1u : 0u;
+                            pop_far = false;
+                        } else {
+                            const bool go_near = t >= exit_t;
+                            const bool go_far = !go_near && t <= entry;
+                            const bool push = !go_near && !go_far;
+                            if (!RESTART) {
+                                st[sp * BLOCK] = (tn << 3) | tp;
+                                sp += push ? 1 : 0;
+                                top_t = push ? t : top_t;
+                            }
+                            exit_t = push ? t : exit_t;
+                            pushed = pushed || push;
+                            c = go_far == pos ? 1u : 0u;
+                        }
+                        if (tp < 3u) {
+                            tp = 2u * tp + 1u + c;
+                            if (RESTART) restart = pushed ? restart : ((tn << 3) | tp);
+                            continue;
+                        }
+                        const uint32_t k = 2u * (tp - 3u) + c;
+                        const uint32_t xb = (r1.w >> 14) & 0xffu;
+                        if ((xb >> k) & 1u) {  // the child treelet
+                            tn = r2.x + (uint32_t)__popc(xb & ((1u << k) - 1u));
+                            tp = 0u;
+                            if (RESTART) restart = pushed ? restart : (tn << 3);
+                        } else {
+                            li = r2.y + (uint32_t)__popc(r2.z & ((1u << (7u + k)) - 1u));
+                            leaf = true;
+                        }
+                        out = true;
+                    }
+                    if (leaf) break;
+                    VC(0, 3);
+                    VL(0, sc.tl + 4 * (size_t)tn, 16, true);
+                    VL(0, sc.tl + 4 * (size_t)tn + 1, 16, true);
+                    VL(0, sc.tl + 4 * (size_t)tn + 2, 16, true);
+                    r0 = sc.tl[4 * (size_t)tn];
+                    r1 = sc.tl[4 * (size_t)tn + 1];
+                    r2 = sc.tl[4 * (size_t)tn + 2];
+                }
+                VC(22, 1);
+                VL(9, sc.tleaf + li, 8, true);
+                nd = sc.tleaf[li];
+            } else {
+            nd = fetch_node(sc, node);
             VC(0, 1);
             VL(0, sc.nodes + node, 8, true);
-            pushed = false;
             while ((nd.y & 3u) != RT_KD_LEAF) {
                 VC(0, 1);
                 // RT_PAIR_FETCH: both children (adjacent, 16 B: one global_load_dwordx4) are
@@ -1016,6 +1001,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                     nd = fetch_node(sc, node);
                 }
             }
+            }
             off = nd.y >> 2;
             cnt = nd.x & LEAF_COUNT_MASK;
             list = off;
@@ -1034,7 +1020,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                     float l;
                     const uint32_t sref = sc.refs[off + j];
                     VL(4, prim_data(sc, sref), 16, true);
-                    const float4 sph = PNT > 0 ? pool_sphere<PNT>(sref & REF_INDEX_MASK) : prim_data(sc, sref)[0];
+                    const float4 sph = prim_data(sc, sref)[0];
                     if (sphere_hit(sph, r, &l) && l >= HIT_MIN)
                         key0 = min(key0, ((unsigned long long)__float_as_uint(l) << 32) | (off + j));
                 }
@@ -1043,14 +1029,25 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             }
         }
         if (!RESTART && !done && sp > 0) {  // the pop after this leaf (if it does not return)
-            VC(1, sp > 1 ? 2 : 1);
-            VL(1, sc.nodes + st[(sp - 1) * BLOCK], 8, true);
-            pop_b = fetch_node(sc, st[(sp - 1) * BLOCK]).y;
-            if (sp > 1) below = fetch_node(sc, st[(sp - 2) * BLOCK]);
+            if (TL) {
+                if (sp > 1) {  // the branch below the popped one: its split word and axis
+                    VC(1, 2);
+                    const uint32_t b = st[(sp - 2) * BLOCK];
+                    const uint32_t* w = reinterpret_cast<const uint32_t*>(sc.tl + 4 * (size_t)(b >> 3));
+                    VL(1, w + (b & 7u), 4, true);
+                    VL(1, w + 7, 4, true);
+                    below = make_uint2(w[b & 7u], (w[7] >> (2u * (b & 7u))) & 3u);
+                }
+            } else {
+                VC(1, sp > 1 ? 2 : 1);
+                VL(1, sc.nodes + st[(sp - 1) * BLOCK], 8, true);
+                pop_b = fetch_node(sc, st[(sp - 1) * BLOCK]).y;
+                if (sp > 1) below = fetch_node(sc, st[(sp - 2) * BLOCK]);
+            }
         }
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
-        const unsigned long long key = coop_leaf<SLAB && (RT_SLAB_TRIS > 0), PNT>(sc, r, off, cnt, lane, key0);
+        const unsigned long long key = coop_leaf(sc, r, off, cnt, lane, key0);
         TM_ADD(12, TM_NOW() - tmc0);
         TM_ADD(13, (__shfl(wave_incl_scan(cnt, lane), 63) + 63u) / 64u);
         if (!done) {
@@ -1068,15 +1065,8 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                 const uint32_t ref = sc.refs[(uint32_t)key];
                 VL(5, sc.refs + (uint32_t)key, 4, true);
                 VL(5, prim_data(sc, ref), 48, true);
-                float4 a0, a1, a2;
-                if constexpr (PNT > 0) {
-                    pool_load<PNT>(sc.n_pool, ref & REF_INDEX_MASK, a0, a1, a2);
-                } else {
-                    const float4* pd = prim_data(sc, ref);
-                    a0 = pd[0];
-                    a1 = pd[1];
-                    a2 = pd[2];
-                }
+                const float4* pd = prim_data(sc, ref);
+                const float4 a0 = pd[0], a1 = pd[1], a2 = pd[2];
                 float l = 0.f, bu = 0.f, bv = 0.f;
                 if ((ref >> REF_KIND_SHIFT) == K_SPHERE) (void)sphere_hit(a0, r, &l);
                 else (void)tri_hit(xyz(a0), xyz(a1), xyz(a2), r, &l, &bu, &bv);
@@ -1233,7 +1223,7 @@ __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax,
 
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
-template <bool RESTART, bool SLAB, int PNT = 0>
+template <bool RESTART, bool TL>
 __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
                                              uint32_t* st, bool active, bool camera = false,
                                              const PkScene* ps = nullptr) {
@@ -1245,7 +1235,7 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     const bool all_fast = __ballot(!fast) == 0;
     bool pk = false, pk_live = false;
     TM_VAR(const unsigned long long tm0 = TM_NOW());
-    if (RT_PACKET && !SLAB && ps && sc.packet) {
+    if (RT_PACKET && ps && sc.packet) {
         // camera rays of the direction octant of the first one form the packet (NaN directions
         // never: d > 0 and d < 0 are both false); the other lanes take the cooperative search
         const uint32_t oct = (ax.dx > 0.0f ? 1u : 0u) | (ax.dy > 0.0f ? 2u : 0u) | (ax.dz > 0.0f ? 4u : 0u);
@@ -1271,9 +1261,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     TM_ADD(8, __popcll(__ballot(in_coop)));
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
-            found = stack_search_coop<true, RESTART, SLAB, PNT>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<true, RESTART, TL>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
         else
-            found = stack_search_coop<false, RESTART, SLAB, PNT>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<false, RESTART, TL>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
     }
     TM_ADD(1, TM_NOW() - tm1);
     if (found) return true;
@@ -1658,8 +1648,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     return ++p.depth >= MAX_BOUNCES;
 }
 
-template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool SLAB = false,
-          int PNT = 0>
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool TL = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true, const PkScene* ps = nullptr) {
     if (COUNT) c.segments++;
@@ -1668,7 +1657,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop<RESTART, SLAB, PNT>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
+    const bool hit = COOP ? closest_coop<RESTART, TL>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
                           : closest<COUNT, GEN, RESTART>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
@@ -1908,27 +1897,16 @@ __device__ __forceinline__ void make_start(const LaunchArgs& a, const DevScene& 
     e[5][lane] = slot;
 }
 
-// PNT > 0: the pool kernel (whole-pool residency, see g_pool4), PNT threads per workgroup; its
-// occupancy is one or two workgroups per CU (queue_lds_bytes), its traversal stackless.
-template <int PNT>
-constexpr int queue_min_waves(bool gen) {
-    return PNT == 768 ? 6 : (PNT == 1024 ? 4 : (gen ? RT_MIN_WAVES_GEN : RT_MIN_WAVES));
-}
-template <bool GEN, bool DLS, bool RESTART, bool SLAB = false, int PNT = 0>
-__global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) void queue_kernel(
+template <bool GEN, bool DLS, bool RESTART, bool TL = false>
+__global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(
     LaunchArgs a, const uint2* __restrict__ pk_nodes, const uint32_t* __restrict__ pk_refs,
     const float4* __restrict__ pk_prim4) {
-    static_assert(PNT == 0 || (GEN && RESTART && !SLAB && !DLS), "the pool kernel is the stackless general one");
-    constexpr uint32_t TPB = PNT > 0 ? (uint32_t)PNT : (uint32_t)BLOCK;  // threads per workgroup
+    constexpr uint32_t TPB = (uint32_t)BLOCK;  // threads per workgroup
     extern __shared__ uint32_t dyn_lds[];
     const DevScene& sc = a.sc;
     TM_VAR(const unsigned long long tm_start = TM_NOW());
     if (!GEN) {  // only the sphere-only kernel reads the LDS sphere tables
         fill_lds_spheres(sc);
-        __syncthreads();
-    }
-    if constexpr (PNT > 0) {  // the whole pool, once per workgroup
-        pool_fill<PNT>(sc);
         __syncthreads();
     }
     uint32_t* st = GEN ? dyn_lds + threadIdx.x
@@ -2082,7 +2060,7 @@ __global__ __launch_bounds__(PNT > 0 ? PNT : BLOCK, queue_min_waves<PNT>(GEN)) v
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
-        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, SLAB, PNT>(sc, p, st, c, have, &ps) && have
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, TL>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             if (GEN) VC(13, 1);
@@ -2160,30 +2138,21 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
 }
 
 // The queue kernel of a launch: sphere-only or general, with direct-light sampling, stackless or
-// with a traversal stack (DevScene::restart: 0 stack, 1 stackless, 2 stackless with the triangle
-// slabs of coop_leaf).  The stack is in LDS for the general kernels and in global memory for the
-// sphere-only one (queue_gstack_bytes); the stackless kernels need neither.
-// The pool kernel (DevScene::pool_nt: 768 or 1024 threads per workgroup) takes precedence over
-// the others; it is only chosen for the general kernel without direct-light sampling.
+// with a traversal stack (DevScene::restart).  The stack is in LDS for the general kernels and in
+// global memory for the sphere-only one (queue_gstack_bytes); the stackless kernels need neither.
 template <class F>
 static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
-    const uint32_t rs = a.sc.restart;
-    if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
+    const bool rs = a.sc.restart != 0;
     if (a.sc.spheres_only) return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
-    if (a.sc.pool_nt == 768) return f(queue_kernel<true, false, true, false, 768>, true);
-    if (a.sc.pool_nt == 1024) return f(queue_kernel<true, false, true, false, 1024>, true);
-    if (rs == 2) return f(queue_kernel<true, false, true, true>, true);
+    if (a.sc.treelet) {
+        if (a.sc.dls) return rs ? f(queue_kernel<true, true, true, true>, true) : f(queue_kernel<true, true, false, true>, true);
+        return rs ? f(queue_kernel<true, false, true, true>, true) : f(queue_kernel<true, false, false, true>, true);
+    }
+    if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
     return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
 }
-static bool pool_kernel(const LaunchArgs& a) { return a.sc.pool_nt && !a.sc.dls && !a.sc.spheres_only; }
-size_t pool_lds_bytes(uint32_t pool_nt, uint32_t n_pool) {
-    return (size_t)pool_nt * sizeof(unsigned long long) + (size_t)n_pool * 36u;
-}
-static size_t queue_lds_bytes(const LaunchArgs& a, bool gen) {
-    if (pool_kernel(a)) return pool_lds_bytes(a.sc.pool_nt, a.sc.n_pool);
-    return (gen && !a.sc.restart) ? stack_lds_bytes(a) : 0;
-}
-uint32_t queue_block_threads(const LaunchArgs& a) { return pool_kernel(a) ? a.sc.pool_nt : (uint32_t)BLOCK; }
+static size_t queue_lds_bytes(const LaunchArgs& a, bool gen) { return (gen && !a.sc.restart) ? stack_lds_bytes(a) : 0; }
+uint32_t queue_block_threads(const LaunchArgs&) { return (uint32_t)BLOCK; }
 
 // Resident workgroups per CU of the queue kernel this scene launches (its registers and LDS
 // stack decide): the queue grid is exactly that many workgroups per CU.

@@ -42,3 +42,43 @@ def test_no_launch_when_not_needed():
     assert launch_cmd([], {}) is None
     assert launch_cmd(["--gpus", "4", "--config-only", "a380"], {}) is None
     assert launch_cmd(["--gpus", "4", "--as-rank", "0/4"], {}) is None
+    assert launch_cmd(["--gpus", "2", "--frame-abi"], {}) is None  # one process, rt_frame_* over 2 devices
+
+
+RANKS_CHILD = r"""
+import json, os, sys
+sys.argv = ["bench.py"]
+sys.path.insert(0, %(root)r)
+import torch.distributed as dist
+import bench
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=%(rank)d, world_size=2)
+rank = dist.get_rank()
+ident = {"rank": rank, "local_rank": rank, "device": rank, "pci_bus_id": "0000:%%02x:00.0" %% (0x11 + rank),
+         "uuid": "u%%d" %% rank, "name": "fake", "visible_devices": None}
+idents = bench.gather_identities(ident, dist, 2)
+print("RESULT " + json.dumps(bench.rank_summary(idents, dist)), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_rank_identities_gathered_over_two_ranks():
+    """The N > 1 line's proof of what ran: every rank's device ordinal and PCI
+    location gathered to every rank over a real 2-rank gloo group, the count of distinct devices and
+    the group's backend and size — the keys bench.py's N-rank line carries."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, "-c", RANKS_CHILD % {"root": ROOT, "port": port, "rank": r}],
+                              cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    res = [json.loads([ln for ln in o.splitlines() if ln.startswith("RESULT ")][0][7:]) for o, _ in outs]
+    assert res[0] == res[1]
+    r = res[0]
+    assert [i["rank"] for i in r["ranks"]] == [0, 1]
+    assert [i["pci_bus_id"] for i in r["ranks"]] == ["0000:11:00.0", "0000:12:00.0"]
+    assert r["distinct_devices"] == 2
+    assert r["dist"] == {"backend": "gloo", "world_size": 2}

@@ -82,8 +82,11 @@ PEER, STRIDED, LINEAR = 1, 2, 3
 ROW = 1200 * 16  # bytes per RGBA f32 row of the 1200-wide walled frame
 
 
-def run(stub, devices, ndev, stripe=0, height=0):
+def run(stub, devices, ndev, stripe=0, height=0, staging=False):
     env = dict(os.environ, LD_PRELOAD=stub)
+    env.pop("RT_DEBUG_FRAME_STAGING", None)
+    if staging:
+        env["RT_DEBUG_FRAME_STAGING"] = "1"
     code = CHILD % {"root": ROOT, "stub": stub, "devices": devices, "ndev": ndev, "stripe": stripe, "height": height}
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
@@ -146,6 +149,24 @@ def test_render_to_target_devices_gathers_per_batch(stub_lib):  # noqa: F811
     kinds = [c[0] for c in r["target_copies"]]
     assert kinds.count(PEER) == 4 and kinds.count(STRIDED) == 8, kinds
     assert [c for c in r["target_copies"] if c[0] == LINEAR and c[2] == 600 * ROW].__len__() == 4
+
+
+def test_forced_staging_on_one_device(stub_lib):  # noqa: F811
+    """RT_DEBUG_FRAME_STAGING=1 with four contexts on ONE device: contexts 1-3 are gathered through
+    the remote branch (a peer copy device 0 -> device 0 into a staging buffer each, before the
+    placements), exactly the copies of four contexts on four devices; without the knob the same
+    contexts make no peer copy."""
+    r = run(stub_lib, [0, 0, 0, 0], 1, staging=True)
+    assert r["create"] == 0, r
+    g = r["gather_copies"]
+    peers = [c for c in g if c[0] == PEER]
+    assert [(c[1], c[2]) for c in peers] == [(0, 150 * ROW)] * 3, peers
+    assert [c[0] for c in g] == [PEER] * 3 + [STRIDED] * 4 + [LINEAR]
+    assert r["stats"]["n_peer_copies"] == 3 and r["stats"]["n_gathers"] == 1
+    kinds = [c[0] for c in r["target_copies"]]  # rt_render_to_target_devices: 4 batches
+    assert kinds.count(PEER) == 12 and kinds.count(STRIDED) == 16, kinds
+    r0 = run(stub_lib, [0, 0, 0, 0], 1)
+    assert [c for c in r0["gather_copies"] if c[0] == PEER] == []
 
 
 def test_bad_arguments(stub_lib):  # noqa: F811

@@ -36,7 +36,7 @@ def test_batches_equal_one_call_per_batch(gpu_available, monkeypatch, scene_name
     n = 80 * 40 + 17 * 9
     ref = _per_batch_frames(sc, tiles, spp, batch)
     if cap:
-        monkeypatch.setenv("RT_DEBUG_RADIANCE_FLOATS", str(3 * n * cap))
+        monkeypatch.setenv("RT_DEBUG_LAUNCH", f"radiance_floats={3 * n * cap}")
     nb = spp // batch
     with render.Context(sc) as c:
         outs = [torch.full((n, 4), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(nb)]
@@ -58,13 +58,13 @@ def test_batches_equal_one_call_per_batch(gpu_available, monkeypatch, scene_name
 
 @pytest.mark.gpu
 def test_render_to_target_groups_reuse_buffers(gpu_available, monkeypatch):
-    """rt_render_to_target with batch groups of 3 (RT_DEBUG_GROUP_ITEMS) and more batches than its
+    """rt_render_to_target with batch groups of 3 (RT_DEBUG_LAUNCH group_items) and more batches than its
     ring of output buffers: every frame the hook sees, in order, equals the synchronous loop's."""
     from rt_amd import render
 
     sc = load_scene("biplane", width=160, height=96)
-    monkeypatch.setenv("RT_DEBUG_GROUP_ITEMS", str(3 * 160 * 96))
-    monkeypatch.setenv("RT_DEBUG_PIPELINE_SLOTS", "2")  # ring = 3 batches x 2 groups < 14 batches
+    # ring = 3 batches x 2 groups < 14 batches
+    monkeypatch.setenv("RT_DEBUG_LAUNCH", f"group_items={3 * 160 * 96},slots=2")
     frames = []
     render.render_to_target(sc, 14, 1, update_hook=lambda t, done: frames.append((done, t.copy())))
     assert [d for d, _ in frames] == list(range(1, 15))

@@ -52,6 +52,13 @@ def test_bench_two_ranks_equal_one(gpu_available, tmp_path, scene, spp):
     assert one["frame_complete"] and two["frame_complete"]
     assert two["n_gpus"] == 2 and two["scaling"] == "strong"
     assert two["config"]["dist_backend"] == "gloo" and "weak" in two and "gather_ms_per_step" in two
+    # what ran: both ranks' devices (here both device 0), the group's backend and size
+    assert [i["rank"] for i in two["ranks"]] == [0, 1] and [i["device"] for i in two["ranks"]] == [0, 0]
+    assert two["distinct_devices"] == 1 and two["dist"] == {"backend": "gloo", "world_size": 2}
+    assert one["ranks"][0]["pci_bus_id"] == two["ranks"][0]["pci_bus_id"]
+    # rank 0's C-ABI leg over the ranks' devices (rt_frame_*, two contexts on device 0)
+    assert two["frame_abi"]["n_parts"] == 2 and two["frame_abi"]["devices"] == [0, 0], two["frame_abi"]
+    assert two["frame_abi"]["value"] > 0
     # strong: both runs render [0, 3 spp) of every pixel (1 warmup + 2 timed steps)
     assert np.array_equal(f1, f2)
     assert (f2[..., 3] == 1.0).all()
@@ -90,3 +97,37 @@ def test_config5_eight_ranks_on_one_gpu(gpu_available, tmp_path):
     assert eight["gather_step"]["frame_sha256"] == one["frame_sha256"]
     assert eight["weak"]["spp_per_rank_step"] == 8
     assert eight["weak"]["frame_sha256"] == one8["frame_sha256"]
+    # rank 0's C-ABI leg: the same split by rt_frame_* (8 contexts on the ranks' device 0)
+    assert eight["frame_abi"]["n_parts"] == 8 and eight["frame_abi"]["stripe_rows"] == 8
+    assert eight["frame_abi"]["frame_sha256"] == one["frame_sha256"]
+
+
+def _bench_frame_abi(tmp_path, devices, extra, env_extra=None, steps=2, warmup=1):
+    args = [sys.executable, "bench.py", "--frame-abi", "--gpus", str(len(devices)), "--frame-devices",
+            ",".join(str(d) for d in devices), "--steps", str(steps), "--warmup", str(warmup), "--no-cpu",
+            "--no-roofline", "--no-configs", "--frame-digest"] + extra
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(env_extra or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(args, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, r.stdout
+    return json.loads(line[0])
+
+
+@pytest.mark.parametrize("staging", [False, True])
+def test_bench_frame_abi_equals_one(gpu_available, tmp_path, staging):
+    """`bench.py --frame-abi --gpus 2` (one process, rt_frame_* with two contexts, here both on
+    device 0; with RT_DEBUG_FRAME_STAGING=1 the second one gathered through the remote-device
+    branch) renders the 1-rank frame bit for bit (sha256), reports the contexts' devices and the
+    gather's peer-copy and placement times."""
+    one, _ = _bench(tmp_path, "one", 1, ["--scene", "walled", "--spp-per-step", "8", "--frame-digest"], dump=False)
+    env = {"RT_DEBUG_FRAME_STAGING": "1"} if staging else None
+    fa = _bench_frame_abi(tmp_path, [0, 0], ["--scene", "walled", "--spp-per-step", "8"], env_extra=env)
+    assert fa["n_gpus"] == 2 and fa["scaling"] == "strong" and fa["config"]["parallelism"] == "frame_abi2"
+    assert fa["frame_complete"] and fa["frame_sha256"] == one["frame_sha256"]
+    r = fa["frame_abi"]
+    assert r["n_parts"] == 2 and r["devices"] == [0, 0] and fa["distinct_devices"] == 1
+    assert r["n_peer_copies"] == (2 if staging else 0)  # one per gather: after the warm-up and the timed steps
+    assert r["place_ms"] >= 0.0 and r["value"] == fa["value"]

@@ -82,3 +82,63 @@ def test_render_to_target_devices_equals_one_device(gpu_available):
     for (_, a), (_, b) in zip(one, many):
         assert np.array_equal(a, b)
     assert np.array_equal(t1, t3)
+
+
+# ---- the remote-device branch (staging buffers, peer copies, event hand-offs) on one GPU ----
+# RT_DEBUG_FRAME_STAGING=1 gathers every context but the first as if it sat on another device:
+# its buffer goes through hipMemcpyPeerAsync (device 0 -> device 0) into a staging buffer on the
+# first device, placement reads the staging buffer, the next render waits for the copy (`copied`)
+# and the next copy waits for the placement (`placed`).  frame.hip:258-310.
+
+@pytest.mark.parametrize("scene,n", [("walled", 2), ("walled", 8), ("triangles", 8)])
+def test_frame_staging_gathers_twice(gpu_available, monkeypatch, scene, n):
+    from rt_amd import render
+
+    monkeypatch.setenv("RT_DEBUG_FRAME_STAGING", "1")
+    loaded = load_scene(scene)
+    with render.Frame(loaded, [0] * n) as f:
+        f.render(0, 2)
+        first = f.gather()
+        f.render(2, 1)
+        f.render(3, 1)
+        second = f.gather()
+        st = f.stats()
+    assert st["n_gathers"] == 2 and st["n_peer_copies"] == 2 * (n - 1), st
+    assert st["peer_copy_ms_max"] > 0.0, st
+    assert np.array_equal(first, one_context(loaded, 0, 2))
+    assert np.array_equal(second, one_context(loaded, 0, 4))
+
+
+def test_config5_split_through_staging(gpu_available, monkeypatch):
+    """BASELINE config 5's 8-way split (spaceship_r1 4096 x 4096, 64 stripes of 8 rows per context)
+    with 7 of the 8 contexts gathered through staging, two gathers in a row."""
+    from rt_amd import render
+
+    monkeypatch.setenv("RT_DEBUG_FRAME_STAGING", "1")
+    loaded = load_scene("spaceship_r1", width=4096, height=4096)
+    ref1 = one_context(loaded, 0, 1)
+    ref2 = one_context(loaded, 0, 2)
+    with render.Frame(loaded, [0] * 8) as f:
+        f.render(0, 1)
+        got1 = f.gather()
+        f.render(1, 1)
+        got2 = f.gather()
+        st = f.stats()
+    assert st["stripe_rows"] == 8 and st["n_gathers"] == 2 and st["n_peer_copies"] == 14, st
+    assert np.array_equal(got1, ref1)
+    assert np.array_equal(got2, ref2)
+
+
+def test_render_to_target_devices_through_staging(gpu_available, monkeypatch):
+    """rt_render_to_target_devices with 3 contexts, 2 of them gathered through staging: every
+    batch's RGBA8 target (three gathers, pipelined) equals rt_render_to_target's."""
+    from rt_amd import render
+
+    monkeypatch.setenv("RT_DEBUG_FRAME_STAGING", "1")
+    loaded = load_scene("triangles")
+    one, many = [], []
+    render.render_to_target(loaded, 6, 2, 0, update_hook=lambda t, d: one.append((d, t.copy())))
+    render.render_to_target_devices(loaded, 6, 2, [0, 0, 0], update_hook=lambda t, d: many.append((d, t.copy())))
+    assert [d for d, _ in one] == [d for d, _ in many] == [2, 4, 6]
+    for (_, a), (_, b) in zip(one, many):
+        assert np.array_equal(a, b)

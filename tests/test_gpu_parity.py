@@ -182,11 +182,11 @@ def test_lanes_per_pixel_bit_invariant(gpu_available, walled, monkeypatch, k, sp
     from rt_amd import render
 
     crops = CROPS[:2] if spp < 100 else [(560, 260, 16, 8)]
-    monkeypatch.setenv("RT_DEBUG_LANES_PER_PIXEL", "1")
+    monkeypatch.setenv("RT_DEBUG_SCHED", "direct:1")
     with render.Context(walled) as c1:
         ref = c1.render(crops, 0, spp)
         ref2 = c1.render(crops, spp, 5)
-    monkeypatch.setenv("RT_DEBUG_LANES_PER_PIXEL", str(k))
+    monkeypatch.setenv("RT_DEBUG_SCHED", f"direct:{k}")
     with render.Context(walled) as ck:
         g = ck.render(crops, 0, spp)
         g2 = ck.render(crops, spp, 5)
@@ -236,10 +236,10 @@ def test_split_queue_launches_bit_invariant(gpu_available, monkeypatch, scene_na
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 40, h // 2 - 20, 80, 40), (w - 33, h - 9, 33, 9)]
     n_pix = 80 * 40 + 33 * 9
-    monkeypatch.delenv("RT_DEBUG_RADIANCE_FLOATS", raising=False)
+    monkeypatch.delenv("RT_DEBUG_LAUNCH", raising=False)
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, spp)
-    monkeypatch.setenv("RT_DEBUG_RADIANCE_FLOATS", str(3 * n_pix * 4))  # 4 samples per launch
+    monkeypatch.setenv("RT_DEBUG_LAUNCH", f"radiance_floats={3 * n_pix * 4}")  # 4 samples per launch
     with render.Context(sc) as cs:
         g = cs.render(tiles, 0, spp)
         n_split = cs.launch_stats()["n_trace_launches"]
@@ -379,11 +379,8 @@ def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, sp
     with render.Context(sc) as c1:
         ref = c1.render(tiles, 0, spp)
     for pipe, cap in (("2", None), ("0", None), ("2", str(3 * n * 2))):  # cap: 2 samples per launch
-        monkeypatch.setenv("RT_DEBUG_PIPELINE", pipe)  # overlapped launches, or each after the last fold
-        if cap:
-            monkeypatch.setenv("RT_DEBUG_RADIANCE_FLOATS", cap)
-        else:
-            monkeypatch.delenv("RT_DEBUG_RADIANCE_FLOATS", raising=False)
+        # overlapped launches, or each after the last fold
+        monkeypatch.setenv("RT_DEBUG_LAUNCH", f"overlap={pipe}" + (f",radiance_floats={cap}" if cap else ""))
         with render.Context(sc) as ca:
             out = torch.full((n, 4), -1.0, dtype=torch.float32, device="cuda:0")
             stream = torch.cuda.current_stream().cuda_stream
@@ -396,8 +393,7 @@ def test_async_pipeline_bit_invariant(gpu_available, monkeypatch, scene_name, sp
         assert np.array_equal(got, ref), (pipe, cap, parity.stats(got, ref))
     # a synchronous call between async ones
     assert spp >= 3 * batch
-    monkeypatch.delenv("RT_DEBUG_RADIANCE_FLOATS", raising=False)
-    monkeypatch.delenv("RT_DEBUG_PIPELINE", raising=False)
+    monkeypatch.delenv("RT_DEBUG_LAUNCH", raising=False)
     with render.Context(sc) as cm:
         out = torch.zeros((n, 4), dtype=torch.float32, device="cuda:0")
         cm.render_device_async(out.data_ptr(), tiles, 0, batch)
@@ -434,30 +430,21 @@ def test_render_to_target_pipelined_equals_batches(gpu_available, scene_name, sp
                                             ("a380", 2)])
 def test_stackless_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scene_name, spp):
     """Stackless kd-restart with push-down (RT_DEBUG_KD_RESTART=1: after a leaf, descend again from the
-    deepest node above the first push, entry = the leaf's exit) and the stackless kernel with the
-    leaves' triangles staged in LDS (RT_DEBUG_KD_RESTART=2) each render the forward oracle's image (the
-    reference's stack traversal, kdtree.rs:66-104), bit for bit, in the queue kernels; so does the
-    pool kernel (RT_DEBUG_POOL: the whole primitive pool resident in LDS)."""
+    deepest node above the first push, entry = the leaf's exit) and the stack traversal
+    (RT_DEBUG_KD_RESTART=0) each render the forward oracle's image (the reference's stack traversal,
+    kdtree.rs:66-104), bit for bit, in the queue kernels."""
     from rt_amd import render
 
     sc = load_scene(scene_name)
     w, h = sc.info.width, sc.info.height
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
     o = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
-    for rs in ("0", "1", "2"):
+    for rs in ("0", "1"):
         monkeypatch.setenv("RT_DEBUG_KD_RESTART", rs)
         with render.Context(sc) as c:
             g = c.render(tiles, 0, spp)
         assert np.array_equal(g, o), (rs, parity.stats(g, o))
     monkeypatch.delenv("RT_DEBUG_KD_RESTART")
-    # the pool kernel (every primitive resident in LDS, stackless), where the pool fits: 768 and
-    # 1024 threads per workgroup (triangles.yml, spaceship_r1; biplane / a380 do not fit: the
-    # request falls back to the general kernel and the image is the same)
-    for pool in ("768", "1024", "auto"):
-        monkeypatch.setenv("RT_DEBUG_POOL", pool)
-        with render.Context(sc) as c:
-            g = c.render(tiles, 0, spp)
-        assert np.array_equal(g, o), (pool, parity.stats(g, o))
 
 
 @pytest.mark.parametrize("scene_name,spp", [("triangles", 4), ("biplane", 3), ("spaceship_r1", 3), ("a380", 2)])
@@ -465,8 +452,7 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
     """Camera-ray packets (closest_packet: scalar-loaded nodes and leaf refs, per-lane
     near / far / push on the lane's own interval, deferred lanes, kd-restart from the packet's
     restart node, hand-over to the cooperative search), the cooperative search alone
-    (RT_DEBUG_PACKET=0), the row-order queue (RT_DEBUG_PIX_BLOCK=1) and the queue's blocks in
-    reverse or centre-first order (RT_DEBUG_PIX_ORDER=1/2) each render the forward oracle's image
+    (RT_DEBUG_PACKET=0) and the row-order queue (RT_DEBUG_PIX_BLOCK=1) each render the forward oracle's image
     (kdtree.rs:66-104), bit for bit, on two tiles and a full frame."""
     from rt_amd import render
 
@@ -475,10 +461,9 @@ def test_packet_traversal_bit_invariant(gpu_available, oracle, monkeypatch, scen
     tiles = [(w // 2 - 64, h // 2 - 32, 128, 64), (0, h - 16, 48, 16)]
     o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
     o_full = oracle.render(sc, [(0, 0, w, h)], 0, 2 * spp, accum=oracle.ACCUM_FORWARD)
-    for cfg in (("1", "8", "0"), ("0", "1", "0"), ("1", "1", "0"), ("0", "8", "0"), ("1", "8", "1"), ("1", "8", "2")):
+    for cfg in (("1", "8"), ("0", "1"), ("1", "1"), ("0", "8")):
         monkeypatch.setenv("RT_DEBUG_PACKET", cfg[0])
         monkeypatch.setenv("RT_DEBUG_PIX_BLOCK", cfg[1])
-        monkeypatch.setenv("RT_DEBUG_PIX_ORDER", cfg[2])
         with render.Context(sc) as c:
             got = c.render(tiles, 0, spp)
         assert np.array_equal(got, o_tiles), (cfg, parity.stats(got, o_tiles))
@@ -502,7 +487,7 @@ def test_queue_shards_bit_invariant(gpu_available, oracle, monkeypatch, scene_na
     o_full = oracle.render(sc, [(0, 0, w, h)], 0, spp, accum=oracle.ACCUM_FORWARD)
     o_tiles = oracle.render(sc, tiles, 0, spp, accum=oracle.ACCUM_FORWARD)
     for n in ("1", "3", "8", "32"):
-        monkeypatch.setenv("RT_DEBUG_QUEUE_SHARDS", n)
+        monkeypatch.setenv("RT_DEBUG_LAUNCH", f"shards={n}")
         with render.Context(sc) as c:
             full = c.render(None, 0, spp)
             got = c.render(tiles, 0, spp)
@@ -524,8 +509,7 @@ def test_small_launch_pipeline_bit_invariant(gpu_available, oracle, monkeypatch)
     spp = 6
     o = oracle.render(sc, [(0, 0, w, h)], 0, spp, accum=oracle.ACCUM_FORWARD)
     for slots, div in (("12", "8"), ("12", "2"), ("3", "16")):
-        monkeypatch.setenv("RT_DEBUG_PIPELINE_SLOTS", slots)
-        monkeypatch.setenv("RT_DEBUG_GRID_DIV", div)
+        monkeypatch.setenv("RT_DEBUG_LAUNCH", f"slots={slots},grid_div={div}")
         with render.Context(sc) as c:
             out = torch.zeros((w * h, 4), dtype=torch.float32, device="cuda:0")
             stream = torch.cuda.current_stream().cuda_stream

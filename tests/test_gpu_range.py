@@ -18,10 +18,10 @@ N_WALLED = 64 * 32 + 9 * 7
 CASES = [
     ("walled", WALLED_TILES, 10, 7, {}),
     ("walled", WALLED_TILES, 10, 7, {"RT_DEBUG_SCHED": "direct"}),                       # lanes per pixel + fold
-    ("walled", WALLED_TILES, 10, 9, {"RT_DEBUG_RADIANCE_FLOATS": str(3 * N_WALLED * 2)}),  # 5 launches
+    ("walled", WALLED_TILES, 10, 9, {"RT_DEBUG_LAUNCH": f"radiance_floats={3 * N_WALLED * 2}"}),  # 5 launches
     ("walled", WALLED_TILES, 0, 5, {}),                                              # range from sample 0
     ("biplane", [(600, 300, 32, 16)], 4, 5, {}),
-    ("biplane", [(600, 300, 32, 16)], 4, 5, {"RT_DEBUG_PIPELINE": "2"}),
+    ("biplane", [(600, 300, 32, 16)], 4, 5, {"RT_DEBUG_LAUNCH": "overlap=2"}),
 ]
 
 

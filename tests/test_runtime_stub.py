@@ -54,7 +54,7 @@ def stub_lib(tmp_path_factory):
 
 
 def run_child(stub, queries):
-    env = dict(os.environ, LD_PRELOAD=stub, RT_DEBUG_PIPELINE_SLOTS="4")
+    env = dict(os.environ, LD_PRELOAD=stub, RT_DEBUG_LAUNCH="slots=4")
     code = CHILD % {"root": ROOT, "stub": stub, "queries": queries}
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
@@ -169,7 +169,7 @@ print("RESULT", json.dumps(res))
 
 def run_slots(stub, scene, queues, cases):
     env = dict(os.environ, LD_PRELOAD=stub, GPU_MAX_HW_QUEUES=str(queues))
-    for k in ("RT_DEBUG_PIPELINE_SLOTS", "RT_DEBUG_GRID_DIV", "RT_DEBUG_PIPELINE", "RT_DEBUG_SMALL_LAUNCH_ITEMS"):
+    for k in ("RT_DEBUG_LAUNCH",):
         env.pop(k, None)
     code = CHILD_SLOTS % {"root": ROOT, "stub": stub, "scene": scene, "cases": cases}
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)

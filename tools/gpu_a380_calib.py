@@ -1,6 +1,6 @@
 """a380 at 1 spp per call (bench config 2's launch shape) through FrameSteps after a long warmup
 (the first ~100 launches of a process run ~25% slower); env knobs of the launch pipeline
-(GPU_MAX_HW_QUEUES, RT_DEBUG_PIPELINE_SLOTS, RT_DEBUG_GRID_DIV) are read per process."""
+(GPU_MAX_HW_QUEUES, RT_DEBUG_LAUNCH slots / grid_div) are read per process."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)

@@ -1,5 +1,5 @@
 """Fixed cost of one queue launch (start-up + drain tail): walled.yml rendered in ONE launch at
-several spp (RT_DEBUG_RADIANCE_GIB raised so that 2000 spp still fit one launch), kernel time from
+several spp (RT_DEBUG_LAUNCH radiance_gib raised so that 2000 spp still fit one launch), kernel time from
 the launch's HIP events; a least-squares line ms = a + b * spp gives the per-launch intercept a.
 Usage: python tools/launch_overhead.py [--scene walled] [--spp 250 500 1000 2000]"""
 import argparse
@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--spp", type=int, nargs="+", default=[250, 500, 1000, 2000])
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
-    os.environ.setdefault("RT_DEBUG_RADIANCE_GIB", "32")
+    os.environ.setdefault("RT_DEBUG_LAUNCH", "radiance_gib=32")
     import numpy as np
     import torch  # noqa: F401  (owns the HIP runtime)
     from rt_amd import render, scheme

@@ -43,7 +43,7 @@ print("SAMPLES", int(loaded.info.width) * int(loaded.info.height) * %(spp)d, flu
 
 
 def gpu(spp):
-    env = dict(os.environ, RT_DEBUG_PIPELINE="0")
+    env = dict(os.environ, RT_DEBUG_LAUNCH="overlap=0")
     r = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "spp": spp}], capture_output=True, text=True,
                        timeout=600, env=env)
     counts, samples, launches = {}, None, None
