@@ -27,8 +27,9 @@ absolute sample index).
 
 Prints ONE JSON line (rank 0).  `roofline` names the measured limiter of the trace kernel:
 VALU issue (SQ_INSTS_VALU per launch over the launch's HIP-event duration, against 256 CUs x
-4 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz), HBM traffic (FETCH_SIZE x 2) or the
-vector-memory return path (TD busy), whichever is the largest fraction.  Counter values come
+4 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz), HBM traffic (FETCH_SIZE x 2) or, for the
+mesh configs, the vector-memory issue and dependent-load latency ceilings of tools/mesh_roofline.py
+(samples/s), whichever is the largest fraction; the texture units' busy fractions ride beside them.  Counter values come
 from the committed rocprofv3 passes (profiles/*_counters.json) of the SAME kernel build — keyed
 on a hash of the library's device code, so a kernel change without a re-profile prints null
 instead of a stale figure.  SURVEY.md §8d's algorithmic bytes of the reference's traversal are
@@ -198,8 +199,22 @@ def min_insts(scene, build_id):
     return d, os.path.relpath(p, ROOT)
 
 
-def roofline(scene, per_launch, kernel_ms, build_id, kernel, kernel_ms_source):
-    """Measured fractions of the trace kernel's ceilings; bound = the largest."""
+def mesh_model(config, build_id, counters, counters_src):
+    """tools/mesh_roofline.py's two ceilings of the general (mesh) kernel on `config`, from the
+    committed load classes of this kernel build (profiles/*_vmem_lines.jsonl) and `counters`."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import mesh_roofline
+
+    v = mesh_roofline.vmem_entry(config, build_id)
+    if not v:
+        return None
+    return mesh_roofline.model_from(v[0], v[1], counters, counters_src)
+
+
+def roofline(scene, per_launch, kernel_ms, build_id, kernel, kernel_ms_source, model_config=None):
+    """Measured fractions of the trace kernel's ceilings; bound = the largest.  For the general
+    (mesh) kernel, `model_config` names its load-class measurement: the vector-memory issue and
+    latency ceilings of tools/mesh_roofline.py join the candidates (mesh roofline)."""
     out = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
            "kernel": kernel, "kernel_ms_avg": round(kernel_ms, 3), "kernel_ms_source": kernel_ms_source,
            "samples_per_launch": round(per_launch), "build_id": build_id, "counters_source": None}
@@ -242,15 +257,33 @@ def roofline(scene, per_launch, kernel_ms, build_id, kernel, kernel_ms_source):
         out["hbm"] = h
         fr["hbm"] = h
     if d.get("td_busy_frac"):
-        # the vector-memory pipeline: fraction of the kernel's cycles the per-CU texture-data unit
-        # (the return path of every global / scratch load) is busy; the mesh kernels' limiter
-        v = {"achieved": d["td_busy_frac"], "peak": 1.0, "unit": "fraction of cycles TD busy",
-             "frac": d["td_busy_frac"], "ta_busy_frac": d.get("ta_busy_frac"),
-             "note": "rocprofv3 TD_TD_BUSY_sum / 256 CUs over GRBM_GUI_ACTIVE / 8 XCDs, own pass"}
+        # the texture units' busy fractions (secondary: a unit with a return outstanding counts as
+        # busy, so a latency-bound kernel keeps TD busy high)
+        v = {"td_busy_frac": d["td_busy_frac"], "ta_busy_frac": d.get("ta_busy_frac"),
+             "note": "rocprofv3 TD_TD_BUSY_sum / TA_TA_BUSY_sum over 256 CUs x GRBM_GUI_ACTIVE / 8 XCDs, own pass; "
+                     "not a bound candidate"}
         if d.get("vmem_rd_per_launch"):
             v["vmem_wave_loads_per_sample"] = round(d["vmem_rd_per_launch"] / per_launch, 2)
-        out["vmem"] = v
-        fr["vmem"] = v
+        out["vmem_units"] = v
+    if model_config:
+        m = mesh_model(model_config, build_id, d, src)
+        if m:
+            ach = per_launch / sec / 1e6
+            for key, what in (("vmem_issue", "vector-memory issue: every load class's wave-loads at the measured "
+                                             "gather cost of its shape (tools/gather_sweep.hip)"),
+                              ("latency", "dependent-load chain: wave-level load steps per sample x unloaded "
+                                          "latency (tools/chase_latency.hip), over the resident waves")):
+                ceil = m[key]["ceiling_Msamples_s"]
+                e = {"achieved": round(ach, 1), "peak": ceil, "unit": "Msamples/s", "frac": round(ach / ceil, 4),
+                     "what": what}
+                e.update({k: v for k, v in m[key].items() if k != "ceiling_Msamples_s"})
+                out[key] = e
+                fr[key] = e
+            out["mesh_model"] = {"sources": m["sources"], "vmem_build_id": m["vmem_build_id"],
+                                 "note": "tools/mesh_roofline.py from committed profiles; achieved = samples per launch / "
+                                         "kernel_ms_avg"}
+        else:
+            out["mesh_model"] = {"note": f"no committed load classes of build {build_id} for {model_config}"}
     if d.get("l2_bytes_per_launch"):
         b = d["l2_bytes_per_launch"]
         out["l2"] = {"achieved": round(b / sec / 1e9, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
@@ -360,9 +393,9 @@ def kernel_label(loaded):
                     and loaded.desc.n_spheres <= 64 and not int(loaded.info.dir_light_samp))
     dls = int(loaded.info.dir_light_samp) != 0
     restart = spheres_only or os.environ.get("RT_DEBUG_KD_RESTART", "0") not in ("0", "")
-    slab = os.environ.get("RT_DEBUG_KD_RESTART") == "2"
+    treelet = not spheres_only and os.environ.get("RT_DEBUG_TREELET", "0") not in ("0", "")
     b = lambda v: "true" if v else "false"  # noqa: E731
-    return f"rtd::queue_kernel<{b(not spheres_only)}, {b(dls)}, {b(restart)}, {b(slab)}>"
+    return f"rtd::queue_kernel<{b(not spheres_only)}, {b(dls)}, {b(restart)}, {b(treelet)}>"
 
 
 def load(scene, width=None, height=None):
@@ -459,7 +492,7 @@ def run_config(name, cpu, build_id, per_batch_calls=True):
     if per_calls is not None:
         res["value_per_batch_calls"] = rate(per_calls)
     res["roofline"] = roofline(scene if name != "spaceship_r1@4096" else "spaceship_r1", per_launch, kms, build_id,
-                               kernel_label(loaded), "one synchronous launch (no overlap)")
+                               kernel_label(loaded), "one synchronous launch (no overlap)", model_config=name)
     if cpu:
         res["cpu_baseline"] = cpu_baseline(loaded, CPU_SPP_MIN_RUN.get(name, CPU_SPP[name]),
                                            rows_step=CPU_ROWS_STEP.get(name, 1))

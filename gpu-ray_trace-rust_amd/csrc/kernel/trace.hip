@@ -1825,9 +1825,12 @@ __device__ __forceinline__ uint32_t grab_size(uint32_t remaining, uint32_t n_wav
 // shard when its own is exhausted; it is done when it has found every shard exhausted (counters
 // only grow).  Shard boundaries are multiples of 64, so a grab (a multiple of 64, at least 64)
 // that starts inside a shard covers every lane that asks.  Which lane traces an item changes,
-// never what the item computes: bit-identical images.  The runtime shards only small scenes
-// (runtime.hip queue_shards): on the mesh scenes one counter, whose waves all work on one
-// window of consecutive items, ran 5-8% faster than 8 shards.
+// never what the item computes: bit-identical images.  The runtime (runtime.hip queue_shards)
+// gives 8 shards to tiny scenes (their grabs serialise on one counter: triangles.yml 4,937 ->
+// 14,120 Msamples/s) and to scenes whose traversal data exceeds one XCD's 4 MiB L2 (each XCD then
+// walks its own window of pixels: a380 +4..11% in synchronous launches); the mid-size meshes keep
+// one counter, whose waves all work on one window of consecutive items (spaceship_r1 and biplane
+// lose 3-8% with shards).
 constexpr uint32_t QSHARD_STRIDE = 32;  // uint32 words between shard counters (128 B)
 __device__ __forceinline__ uint32_t qshard_begin(const LaunchArgs& a, uint32_t k) {
     if (k == 0) return 0u;

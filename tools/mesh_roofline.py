@@ -54,9 +54,6 @@ def gather_table():
     return out
 
 
-SWEEP_KIND = {"dword": "dword", "dwordx2": "dwordx2", "dwordx4": "dwordx4", "tri48": "tri48"}
-
-
 def sweep_table():
     """{(kind, level, active_lanes): [(lines per wave-load, ns per wave-load chip-wide)]} from the
     committed gather sweep (tools/gather_sweep.hip), or None when there is none."""
@@ -104,15 +101,22 @@ def chase_latency():
     return {"L1": rnd[8192], "L2": rnd[3145728], "MALL": rnd[33554432]}
 
 
-def latest(pattern, scene, key="scene"):
+def vmem_entry(config, build_id=None):
+    """The latest committed load-class measurement of `config` (tools/vmem_classes.py; spaceship_r1@4096
+    for the 4096 x 4096 frame), of the product build `build_id` when given."""
     best = None
-    for p in sorted(glob.glob(os.path.join(PROF, pattern))):
+    for p in sorted(glob.glob(os.path.join(PROF, "*_vmem_lines.jsonl"))):
         for line in open(p):
             if not line.strip():
                 continue
             d = json.loads(line)
-            if d.get(key) == scene:
-                best = (d, os.path.relpath(p, ROOT))
+            if d.get("config", d.get("scene")) != config or "lines_by_class" not in d:
+                continue
+            if build_id is not None and d.get("build_id") != build_id:
+                continue
+            if d.get("treelet", "0") not in ("0", ""):
+                continue  # a run of the off-default treelet descent
+            best = (d, os.path.relpath(p, ROOT))
     return best
 
 
@@ -125,13 +129,8 @@ def counters_for(scene, build_id=None):
     return best
 
 
-def model(scene, vmem_file=None, build_id=None):
-    v = latest(vmem_file or "*_vmem_lines.jsonl", scene)
-    c = counters_for(scene, build_id)
-    if not v or not c:
-        return None
-    vl, vsrc = v
-    cnt, csrc = c
+def model_from(vl, vsrc, cnt, csrc):
+    """The two ceilings from one load-class measurement (vl) and the product build's counters (cnt)."""
     per, cls = vl["per_sample"], vl["lines_by_class"]
     gt = gather_table()
     sw, sw_src = sweep_table()
@@ -156,7 +155,7 @@ def model(scene, vmem_file=None, build_id=None):
         classes[name] = {"wave_loads": wl, "kind": kind, "lines_per_wave_load": round(n, 2),
                          "active_lanes": round(lanes, 1),
                          "ns_L1": round(t1, 5), "ns_L2": round(t2, 5), "ns_per_sample": round(t, 4)}
-    tl = "leaf_rec" in per and per.get("leaf_rec", 0) > 0
+    tl = per.get("leaf_rec", 0.0) > 0
     steps = {"descent": per["descent"] / 3.0 + per.get("leaf_rec", 0.0) if tl else per["descent"],
              "passes": 2.0 * per["passes"], "retest": 2.0 * per["retest"] / 4.0, "lead_sph": per["lead_sph"],
              "pixq": per["pixq"], "mesh_rec": per["mesh_rec"], "tex": per["tex"]}
@@ -164,7 +163,7 @@ def model(scene, vmem_file=None, build_id=None):
     lat = chase_latency()
     l2h = cnt.get("l2_hit_rate") or 0.0
     lat_ns = h1 * lat["L1"] + (1 - h1) * (l2h * lat["L2"] + (1 - l2h) * lat["MALL"])
-    return {"scene": scene,
+    return {"config": vl.get("config", vl.get("scene")),
             "vmem_issue": {"ns_per_sample": round(t_v, 4), "ceiling_Msamples_s": round(1e3 / t_v, 1),
                            "l1_line_hit_frac": round(h1, 4), "l2_requests_per_sample": round(l2_req, 2),
                            "distinct_lines_per_sample": round(lines_total, 2), "classes": classes},
@@ -176,14 +175,23 @@ def model(scene, vmem_file=None, build_id=None):
             "sources": {"vmem_classes": vsrc, "counters": csrc,
                         "gather_rates": sw_src if sw else "profiles/r2_gather_rates.json",
                         "chase_latency": "profiles/r5_chase_latency.jsonl"},
-            "counters_build_id": cnt.get("build_id"), "vmem_spp_per_launch": vl.get("spp_per_launch")}
+            "counters_build_id": cnt.get("build_id"), "vmem_build_id": vl.get("build_id"),
+            "vmem_spp_per_launch": vl.get("spp_per_launch")}
+
+
+def model(config, build_id=None):
+    scene = config.split("@")[0]
+    v = vmem_entry(config, build_id)
+    c = counters_for(scene, build_id)
+    if not v or not c:
+        return None
+    return model_from(v[0], v[1], c[0], c[1])
 
 
 def main(argv):
-    vmem_file = argv[0] if argv else None
-    for scene in ("a380", "biplane", "spaceship_r1"):
-        m = model(scene, vmem_file)
-        print(json.dumps(m if m else {"scene": scene, "error": "no vmem classes or counters"}), flush=True)
+    for config in argv or ("a380", "biplane", "spaceship_r1@4096", "triangles"):
+        m = model(config)
+        print(json.dumps(m if m else {"config": config, "error": "no load classes or counters"}), flush=True)
 
 
 if __name__ == "__main__":

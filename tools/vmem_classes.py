@@ -3,7 +3,9 @@ RT_VMEM_COUNT diagnostic build: make -C gpu-ray_trace-rust_amd diag -> lib/varia
 Renders one full-frame launch of each scene in a child process (the kernel's printf goes to the
 child's stdout) and prints one JSON line per scene: wave-level load instructions per sample by
 class, next to SQ_INSTS_VMEM_RD per sample from the committed counters of the product build.
-Usage (on the GPU box): python tools/vmem_classes.py [scene:spp ...] > profiles/<tag>_vmem_classes.jsonl"""
+Usage (on the GPU box): python tools/vmem_classes.py [scene[@N]:spp ...] > profiles/<tag>_vmem_lines.jsonl
+(@N: an N x N frame; each line carries the product build id of the same source, which bench.py's
+mesh roofline requires to match)"""
 import json
 import os
 import re
@@ -27,7 +29,7 @@ import torch  # noqa: F401
 from rt_amd import abi, render, scheme
 lib = abi.load_library(os.path.join(%(root)r, "gpu-ray_trace-rust_amd", "lib", "variants", "librt_diag_vmem.so"))
 sch = scheme.load_json(os.path.join(%(root)r, "tests", "golden", "scenes", %(scene)r + ".json"))
-loaded = scheme.load(sch, assets_root=os.path.join(%(root)r, "assets_pack"), lib=lib)
+loaded = scheme.load(sch, assets_root=os.path.join(%(root)r, "assets_pack"), lib=lib, width=%(width)s, height=%(width)s)
 with render.Context(loaded, lib=lib) as c:
     c.render(None, 0, %(spp)d, want_output=False)
     c.render(None, %(spp)d, %(spp)d, want_output=False)
@@ -36,10 +38,16 @@ print("PIXELS", int(loaded.info.width) * int(loaded.info.height), flush=True)
 
 
 def main(specs):
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ray_trace-rust_amd"))
+    from rt_amd import abi
+
+    build_id = abi.kernel_build_id()  # the product library built from the same source
     for spec in specs:
-        scene, _, spp = spec.partition(":")
+        # scene[@N]:spp — @N renders at N x N (spaceship_r1@4096: BASELINE config 5's frame)
+        config, _, spp = spec.partition(":")
+        scene, _, size = config.partition("@")
         spp = int(spp or 10)
-        code = CHILD % {"root": ROOT, "scene": scene, "spp": spp}
+        code = CHILD % {"root": ROOT, "scene": scene, "spp": spp, "width": int(size) if size else None}
         # serialized launches: the counters are per launch (overlapped launches would mix them)
         env = dict(os.environ, RT_DEBUG_LAUNCH="overlap=0")
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, env=env)
@@ -58,7 +66,8 @@ def main(specs):
         g = {k: last[15 + i] for i, k in enumerate(gn)}
         samples = pix * spp  # the second launch (the first warms up; each launch prints its own)
         per = {k: round(d[k] / samples, 3) for k in NAMES + list(EXTRA.values())}
-        out = {"scene": scene, "spp_per_launch": spp, "samples": samples, "per_sample": per,
+        out = {"scene": scene, "config": config, "build_id": build_id, "treelet": os.environ.get("RT_DEBUG_TREELET", "0"),
+               "spp_per_launch": spp, "samples": samples, "per_sample": per,
                "vmem_loads_per_sample": round(sum(d[k] for k in LOADS) / samples, 2)}
         if g.get("pairs"):
             # cooperative pairs by the number of the wave's lanes at the same leaf in that round
