@@ -393,9 +393,8 @@ def kernel_label(loaded):
                     and loaded.desc.n_spheres <= 64 and not int(loaded.info.dir_light_samp))
     dls = int(loaded.info.dir_light_samp) != 0
     restart = spheres_only or os.environ.get("RT_DEBUG_KD_RESTART", "0") not in ("0", "")
-    treelet = not spheres_only and os.environ.get("RT_DEBUG_TREELET", "0") not in ("0", "")
     b = lambda v: "true" if v else "false"  # noqa: E731
-    return f"rtd::queue_kernel<{b(not spheres_only)}, {b(dls)}, {b(restart)}, {b(treelet)}>"
+    return f"rtd::queue_kernel<{b(not spheres_only)}, {b(dls)}, {b(restart)}>"
 
 
 def load(scene, width=None, height=None):

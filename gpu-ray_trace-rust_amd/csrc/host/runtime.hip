@@ -24,7 +24,6 @@
 #include "../kernel/device_scene.h"
 #include "host_internal.h"
 #include "mesh_flatten.h"
-#include "treelet.h"
 
 using namespace rtd;
 using namespace rth;
@@ -467,14 +466,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         n.x |= lead << LEAF_LEAD_SHIFT;
     }
 
-    // The cooperative descent's treelets (treelet.h): the same tree, three levels per record.
-    std::vector<uint32_t> tl_words, tl_leaves;
-    {
-        std::vector<uint32_t> flat(2 * nodes.size());
-        for (size_t i = 0; i < nodes.size(); ++i) flat[2 * i] = nodes[i].x, flat[2 * i + 1] = nodes[i].y;
-        if (!build_treelets(flat, &tl_words, &tl_leaves)) return set_err(c, RT_ERR_UNSUPPORTED, "KD tree too large for treelets");
-    }
-
     // Direct-light sampling (radiance.rs:89-120): every AABB'd renderable as a device ref in
     // renderable order (the shadow ray's brute-force closest_ray_hit), and the emissive spheres
     // with their position in that list.  Cube maps hit at +inf and can never be a shadow ray's
@@ -574,14 +565,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     d.n_emit = (uint32_t)emit.size();
     d.dls = emit.empty() ? 0u : 1u;  // no emitter: the DLS term is exactly zero
     if ((st = upload(c, refs, &d.refs))) return st;
-    {
-        std::vector<uint4> tl4(tl_words.size() / 4);
-        std::memcpy(tl4.data(), tl_words.data(), tl_words.size() * sizeof(uint32_t));
-        std::vector<uint2> tlf(tl_leaves.size() / 2);
-        std::memcpy(tlf.data(), tl_leaves.data(), tl_leaves.size() * sizeof(uint32_t));
-        if ((st = upload(c, tl4, &d.tl))) return st;
-        if ((st = upload(c, tlf, &d.tleaf))) return st;
-    }
     if ((st = upload(c, sph, &d.sph))) return st;
     if ((st = upload(c, sph_mat, &d.sph_mat))) return st;
     {   // the leaf-test pool: spheres, free triangles, mesh triangles, 3 float4 each
@@ -747,11 +730,6 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
     }
     d.restart = d.spheres_only ? 1u : 0u;
     if (const char* e = debug_env("KD_RESTART")) d.restart = std::strcmp(e, "0") ? 1u : 0u;
-    // The cooperative descent over treelets (trace.hip stack_search_coop TL), RT_DEBUG_TREELET=1;
-    // the default descends over the nodes, a child pair per level (treelets measured 19-27%
-    // slower).
-    d.treelet = 0u;
-    if (const char* e = debug_env("TREELET")) d.treelet = d.tl && std::strcmp(e, "0") ? 1u : 0u;
     // Overlapped launches pay off while a launch's drain tail is a sizeable share of it: mesh
     // launches (8-10 ms tails) and small sphere-only ones — walled's ~0.4 ms tail on
     // one rank's 90 M-sample share at N = 8 (9 ms): +3% overlapped, while at 180 M it is neutral

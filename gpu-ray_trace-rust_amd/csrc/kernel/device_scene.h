@@ -75,13 +75,6 @@ struct DevScene {
     uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
     uint32_t restart;       // queue kernels: 0 stack, 1 stackless (kd-restart with push-down)
     uint32_t packet;        // general queue kernel: camera rays may be traced as packets (closest_packet)
-    // The same tree as 3-level treelets (host/treelet.h): 64-B records (tl, 4 x uint4 each, the
-    // first three loaded) and the leaves reached from them (tleaf, the node layout), read by the
-    // cooperative descent when `treelet` is set; a stack entry or restart point is a treelet
-    // index << 3 | position.
-    const uint4* tl;
-    const uint2* tleaf;
-    uint32_t treelet;
     float bounds[6];
     // spheres
     const float4* sph;      // c.xyz, r

@@ -812,28 +812,14 @@ __device__ __forceinline__ unsigned long long coop_leaf(const DevScene& sc, cons
 // whose t is strictly larger, go near again with exit = their t, as their stack entries would
 // have left it.  The remaining interval is empty exactly when the descent pushed nothing
 // (exit == root exit), the reference's empty stack.
-// Split bits of treelet position p (0..6) from the record's first seven words (treelet.h).
-__device__ __forceinline__ uint32_t sel7(uint4 a, uint4 b, uint32_t p) {
-    const bool b0 = (p & 1u) != 0u, b1 = (p & 2u) != 0u, b2 = (p & 4u) != 0u;
-    const uint32_t x01 = b0 ? a.y : a.x, x23 = b0 ? a.w : a.z, x45 = b0 ? b.y : b.x;
-    const uint32_t lo = b1 ? x23 : x01, hi = b1 ? b.z : x45;
-    return b2 ? hi : lo;
-}
-
-// TL (treelets, DevScene::tl): the descent reads the tree as 3-level treelets (host/treelet.h):
-// one 48-B load brings the splits and axes of a branch and the two levels below it, so a lane
-// decides up to three levels per dependent load instead of one (the node layout's child-pair
-// load per level).  The branches met, their order and their split values are the node tree's:
-// `node` is then a treelet index << 3 | position (stack entries and the restart point too), and
-// the pop resumes at the pushed branch with its far child forced (pop_far).
-template <bool FAST, bool RESTART, bool TL>
+template <bool FAST, bool RESTART>
 __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray& r, const RayAx& ax,
                                                   bool active, float root_entry, float root_exit, Hit* best,
                                                   uint32_t* st) {
     float entry = root_entry, exit_t = root_exit, top_t = root_exit;
     uint32_t node = 0, restart = 0;
     int sp = 0;
-    bool done = !active, found = false, pushed = false, pop_far = false;
+    bool done = !active, found = false, pushed = false;
     const uint32_t lane = __lane_id();
     // RT_LEAF_REUSE: the previous leaf's list (its offset in sc.refs: the upload gives identical
     // lists one copy, so equal offsets mean equal lists) and its minimum key
@@ -844,9 +830,7 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
     // !RESTART: the pop after a leaf that does not return needs two nodes, the branch it returns to
     // (its b word: children and axis) and the branch below it (the new exit); both are loaded ahead
     // of the leaf's passes, so their trip to L1 / L2 overlaps the passes instead of following them
-    // (A/B at 4-10 spp: a380 and biplane +4..7%, spaceship +-0; the bench configs +-0).  TL: the
-    // popped branch's treelet is the next descent's first load, so only the branch below it (its
-    // split word and axis) is loaded ahead.
+    // (A/B at 4-10 spp: a380 and biplane +4..7%, spaceship +-0; the bench configs +-0)
     uint32_t pop_b = 0;
     uint2 below = make_uint2(0u, 0u);
     auto advance = [&]() -> bool {
@@ -859,13 +843,8 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             --sp;
             // the popped branch's node and the one below it were loaded before the leaf's passes
             float d;
-            if (TL) {
-                node = st[sp * BLOCK];
-                pop_far = true;
-            } else {
-                (void)split_t<FAST>(make_uint2(0u, pop_b), ax, r, &d);
-                node = (pop_b >> 2) + (d > 0.0f ? 1u : 0u);
-            }
+            (void)split_t<FAST>(make_uint2(0u, pop_b), ax, r, &d);
+            node = (pop_b >> 2) + (d > 0.0f ? 1u : 0u);
             entry = top_t;
             if (sp) {
                 top_t = split_t<FAST>(below, ax, r, &d);
@@ -881,86 +860,8 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
         unsigned long long key0 = ~0ull;
         VC(12, 1);
         if (!done) {
-            uint2 nd;
+            uint2 nd = fetch_node(sc, node);
             pushed = false;
-            if constexpr (TL) {
-                // the lane's treelet and position; r0 / r1 / r2 its record's words 0-11
-                uint32_t tn = node >> 3, tp = node & 7u;
-                VC(0, 3);
-                VL(0, sc.tl + 4 * (size_t)tn, 16, true);
-                VL(0, sc.tl + 4 * (size_t)tn + 1, 16, true);
-                VL(0, sc.tl + 4 * (size_t)tn + 2, 16, true);
-                uint4 r0 = sc.tl[4 * (size_t)tn], r1 = sc.tl[4 * (size_t)tn + 1], r2 = sc.tl[4 * (size_t)tn + 2];
-                uint32_t li = 0;
-                // One treelet per iteration: up to three levels decided from the record in
-                // registers (no load between them: positions 0 -> 1..2 -> 3..6 -> an exit), then
-                // one load, the child treelet's record or the leaf's.  Lanes out of phase (one
-                // starting at position 5, another at 0) still share each iteration's single load
-                // latency; a level-per-iteration loop paid one latency per level whenever any lane
-                // of the wave crossed into a new treelet (round 6: -23..-25%, profiles/r6_ab).
-                for (;;) {
-                    bool leaf = false, out = false;
-#pragma unroll
-                    for (int step = 0; step < 3; ++step) {
-                        if (out) continue;
-                        const uint32_t tag = (r1.w >> (2u * tp)) & 3u;
-                        if (tag == RT_KD_LEAF) {  // a leaf inside the treelet
-                            li = r2.y + (uint32_t)__popc(r2.z & ((1u << tp) - 1u));
-                            leaf = out = true;
-                            continue;
-                        }
-                        const uint2 bn = make_uint2(sel7(r0, r1, tp), tag);
-                        float d;
-                        const float t = split_t<FAST>(bn, ax, r, &d);
-                        const bool pos = d > 0.0f;
-                        uint32_t c;
-                        if (!RESTART && pop_far) {  // the popped branch: its far child (kdtree.rs:99-102)
-                            c = pos ? 1u : 0u;
-                            pop_far = false;
-                        } else {
-                            const bool go_near = t >= exit_t;
-                            const bool go_far = !go_near && t <= entry;
-                            const bool push = !go_near && !go_far;
-                            if (!RESTART) {
-                                st[sp * BLOCK] = (tn << 3) | tp;
-                                sp += push ? 1 : 0;
-                                top_t = push ? t : top_t;
-                            }
-                            exit_t = push ? t : exit_t;
-                            pushed = pushed || push;
-                            c = go_far == pos ? 1u : 0u;
-                        }
-                        if (tp < 3u) {
-                            tp = 2u * tp + 1u + c;
-                            if (RESTART) restart = pushed ? restart : ((tn << 3) | tp);
-                            continue;
-                        }
-                        const uint32_t k = 2u * (tp - 3u) + c;
-                        const uint32_t xb = (r1.w >> 14) & 0xffu;
-                        if ((xb >> k) & 1u) {  // the child treelet
-                            tn = r2.x + (uint32_t)__popc(xb & ((1u << k) - 1u));
-                            tp = 0u;
-                            if (RESTART) restart = pushed ? restart : (tn << 3);
-                        } else {
-                            li = r2.y + (uint32_t)__popc(r2.z & ((1u << (7u + k)) - 1u));
-                            leaf = true;
-                        }
-                        out = true;
-                    }
-                    if (leaf) break;
-                    VC(0, 3);
-                    VL(0, sc.tl + 4 * (size_t)tn, 16, true);
-                    VL(0, sc.tl + 4 * (size_t)tn + 1, 16, true);
-                    VL(0, sc.tl + 4 * (size_t)tn + 2, 16, true);
-                    r0 = sc.tl[4 * (size_t)tn];
-                    r1 = sc.tl[4 * (size_t)tn + 1];
-                    r2 = sc.tl[4 * (size_t)tn + 2];
-                }
-                VC(22, 1);
-                VL(9, sc.tleaf + li, 8, true);
-                nd = sc.tleaf[li];
-            } else {
-            nd = fetch_node(sc, node);
             VC(0, 1);
             VL(0, sc.nodes + node, 8, true);
             while ((nd.y & 3u) != RT_KD_LEAF) {
@@ -1001,7 +902,6 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
                     nd = fetch_node(sc, node);
                 }
             }
-            }
             off = nd.y >> 2;
             cnt = nd.x & LEAF_COUNT_MASK;
             list = off;
@@ -1029,21 +929,10 @@ __device__ __forceinline__ bool stack_search_coop(const DevScene& sc, const Ray&
             }
         }
         if (!RESTART && !done && sp > 0) {  // the pop after this leaf (if it does not return)
-            if (TL) {
-                if (sp > 1) {  // the branch below the popped one: its split word and axis
-                    VC(1, 2);
-                    const uint32_t b = st[(sp - 2) * BLOCK];
-                    const uint32_t* w = reinterpret_cast<const uint32_t*>(sc.tl + 4 * (size_t)(b >> 3));
-                    VL(1, w + (b & 7u), 4, true);
-                    VL(1, w + 7, 4, true);
-                    below = make_uint2(w[b & 7u], (w[7] >> (2u * (b & 7u))) & 3u);
-                }
-            } else {
-                VC(1, sp > 1 ? 2 : 1);
-                VL(1, sc.nodes + st[(sp - 1) * BLOCK], 8, true);
-                pop_b = fetch_node(sc, st[(sp - 1) * BLOCK]).y;
-                if (sp > 1) below = fetch_node(sc, st[(sp - 2) * BLOCK]);
-            }
+            VC(1, sp > 1 ? 2 : 1);
+            VL(1, sc.nodes + st[(sp - 1) * BLOCK], 8, true);
+            pop_b = fetch_node(sc, st[(sp - 1) * BLOCK]).y;
+            if (sp > 1) below = fetch_node(sc, st[(sp - 2) * BLOCK]);
         }
         DIAG_ROUND_SHARING(off, cnt);
         TM_VAR(const unsigned long long tmc0 = TM_NOW());
@@ -1223,7 +1112,7 @@ __device__ bool closest_packet(const PkScene& ps, const Ray& r, const RayAx& ax,
 
 // closest() for the general queue kernel: called by every lane of the wave; `active` lanes
 // have a ray.
-template <bool RESTART, bool TL>
+template <bool RESTART>
 __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, Hit* best,
                                              uint32_t* st, bool active, bool camera = false,
                                              const PkScene* ps = nullptr) {
@@ -1261,9 +1150,9 @@ __device__ __forceinline__ bool closest_coop(const DevScene& sc, const Ray& r, H
     TM_ADD(8, __popcll(__ballot(in_coop)));
     if (__ballot(in_coop)) {
         if (__builtin_expect(all_fast, 1))
-            found = stack_search_coop<true, RESTART, TL>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<true, RESTART>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
         else
-            found = stack_search_coop<false, RESTART, TL>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
+            found = stack_search_coop<false, RESTART>(sc, r, ax, in_coop, root_entry, root_exit, best, st) || found;
     }
     TM_ADD(1, TM_NOW() - tm1);
     if (found) return true;
@@ -1648,7 +1537,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, Path& p, Hit h, bool h
     return ++p.depth >= MAX_BOUNCES;
 }
 
-template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false, bool TL = false>
+template <bool COUNT, bool GEN, bool DLS = false, bool COOP = false, bool RESTART = false>
 __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* st,
                                         Ctr<COUNT>& c, bool active = true, const PkScene* ps = nullptr) {
     if (COUNT) c.segments++;
@@ -1657,7 +1546,7 @@ __device__ __forceinline__ bool segment(const DevScene& sc, Path& p, uint32_t* s
     // the reference does, just later).
     p.ray.d = normalize(p.ray.d);
     Hit h;
-    const bool hit = COOP ? closest_coop<RESTART, TL>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
+    const bool hit = COOP ? closest_coop<RESTART>(sc, p.ray, &h, st, active, !DLS && p.depth == 0, ps)
                           : closest<COUNT, GEN, RESTART>(sc, p.ray, &h, st, c);
     if (COOP && !active) return false;
     return shade<COUNT, GEN, DLS>(sc, p, h, hit, c);
@@ -1900,7 +1789,7 @@ __device__ __forceinline__ void make_start(const LaunchArgs& a, const DevScene& 
     e[5][lane] = slot;
 }
 
-template <bool GEN, bool DLS, bool RESTART, bool TL = false>
+template <bool GEN, bool DLS, bool RESTART>
 __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(
     LaunchArgs a, const uint2* __restrict__ pk_nodes, const uint32_t* __restrict__ pk_refs,
     const float4* __restrict__ pk_prim4) {
@@ -2063,7 +1952,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
         }
         // the cooperative traversal needs every lane of the wave: lanes without a path help
         const PkScene ps{pk_nodes, pk_refs, pk_prim4};
-        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART, TL>(sc, p, st, c, have, &ps) && have
+        const bool fin = GEN ? segment<false, GEN, DLS, GEN, RESTART>(sc, p, st, c, have, &ps) && have
                              : have && segment<false, GEN, DLS, false, RESTART>(sc, p, st, c);
         if (fin) {
             if (GEN) VC(13, 1);
@@ -2147,10 +2036,6 @@ template <class F>
 static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
     const bool rs = a.sc.restart != 0;
     if (a.sc.spheres_only) return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
-    if (a.sc.treelet) {
-        if (a.sc.dls) return rs ? f(queue_kernel<true, true, true, true>, true) : f(queue_kernel<true, true, false, true>, true);
-        return rs ? f(queue_kernel<true, false, true, true>, true) : f(queue_kernel<true, false, false, true>, true);
-    }
     if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
     return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
 }

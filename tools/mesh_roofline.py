@@ -11,7 +11,7 @@
    h1 = 1 - (L2 requests per sample, rocprofv3 TCC counters of the product build) / (distinct lines
    per sample):  T_v = sum_c wl_c (h1 / R_L1(c) + (1 - h1) / R_L2(c)),  ceiling_v = 1 / T_v.
 2. Latency.  Each wave runs its cooperative rounds as a chain of dependent loads: per sample S
-   wave-level steps (a descent load per node level, or per treelet plus one leaf record; two per
+   wave-level steps (a descent load per node level; two per
    cooperative pass, ref then triangle; two per winner re-test and leading-sphere test; one per
    path start, shading record and texel fetch), each at least the unloaded latency of one
    dependent load (tools/chase_latency.hip, profiles/r5_chase_latency.jsonl: random lanes, 8 KiB /
@@ -31,7 +31,7 @@ PROF = os.path.join(ROOT, "profiles")
 
 # record kind of each load class: bytes per lane of one wave-load (trace.hip)
 KIND = {"descent": "dwordx4", "pop": "dwordx2", "pass_ref": "dword", "pass_tri": "dwordx4", "lead_sph": "dwordx4",
-        "retest": "dwordx4", "pixq": "dwordx4", "mesh_rec": "dwordx4", "tex": "dword", "leaf_rec": "dwordx2"}
+        "retest": "dwordx4", "pixq": "dwordx4", "mesh_rec": "dwordx4", "tex": "dword"}
 # distinct 128-B lines of one "runs16" wave-load (4 runs of 16 consecutive records)
 RUNS16_LINES = {"dword": 4, "dwordx2": 4, "dwordx3": 8, "dwordx4": 8}
 RESIDENT_WAVES = 256 * 4 * 8  # general queue kernel: 8 waves per SIMD (RT_MIN_WAVES_GEN)
@@ -115,7 +115,7 @@ def vmem_entry(config, build_id=None):
             if build_id is not None and d.get("build_id") != build_id:
                 continue
             if d.get("treelet", "0") not in ("0", ""):
-                continue  # a run of the off-default treelet descent
+                continue  # round 6's treelet experiment (profiles/r6_ab/treelet_*), not the product kernel
             best = (d, os.path.relpath(p, ROOT))
     return best
 
@@ -155,8 +155,7 @@ def model_from(vl, vsrc, cnt, csrc):
         classes[name] = {"wave_loads": wl, "kind": kind, "lines_per_wave_load": round(n, 2),
                          "active_lanes": round(lanes, 1),
                          "ns_L1": round(t1, 5), "ns_L2": round(t2, 5), "ns_per_sample": round(t, 4)}
-    tl = per.get("leaf_rec", 0.0) > 0
-    steps = {"descent": per["descent"] / 3.0 + per.get("leaf_rec", 0.0) if tl else per["descent"],
+    steps = {"descent": per["descent"],
              "passes": 2.0 * per["passes"], "retest": 2.0 * per["retest"] / 4.0, "lead_sph": per["lead_sph"],
              "pixq": per["pixq"], "mesh_rec": per["mesh_rec"], "tex": per["tex"]}
     s = sum(steps.values())
@@ -171,7 +170,6 @@ def model_from(vl, vsrc, cnt, csrc):
                         "ns_per_step": round(lat_ns, 2), "resident_waves": RESIDENT_WAVES,
                         "ceiling_Msamples_s": round(RESIDENT_WAVES / (s * lat_ns) * 1e3, 1),
                         "latency_ns": lat, "l2_hit_rate": l2h},
-            "treelet_descent": tl,
             "sources": {"vmem_classes": vsrc, "counters": csrc,
                         "gather_rates": sw_src if sw else "profiles/r2_gather_rates.json",
                         "chase_latency": "profiles/r5_chase_latency.jsonl"},

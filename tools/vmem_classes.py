@@ -15,12 +15,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade",
          "pk_leaves", "passes", "rounds", "rad_stores", "starts"]
-# class 22: the treelet descent's leaf records (trace.hip stack_search_coop TL; 0 in the node descent)
-EXTRA = {22: "leaf_rec"}
-LOADS = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade",
-         "leaf_rec"]
+LOADS = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "sph_shade"]
 # RT_VL classes (diag.h VL): lines / sectors / asked bytes of the load sites by class
-VL_NAMES = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex", "leaf_rec"]
+VL_NAMES = ["descent", "pop", "pass_ref", "pass_tri", "lead_sph", "retest", "pixq", "mesh_rec", "tex"]
 
 CHILD = r"""
 import os, sys
@@ -61,12 +58,11 @@ def main(specs):
         vl = [l.split() for l in r.stdout.splitlines() if l.startswith("RT_VL ")]
         vl_last = {int(x[1]): [int(v) for v in x[2:6]] for x in vl[-16:]} if len(vl) >= 32 else {}
         d = {k: last[i] for i, k in enumerate(NAMES)}
-        d.update({k: last.get(i, 0) for i, k in EXTRA.items()})
         gn = ["pairs", "pairs_g2", "pairs_g3", "pairs_g4", "pairs_g8", "quads", "groups"]
         g = {k: last[15 + i] for i, k in enumerate(gn)}
         samples = pix * spp  # the second launch (the first warms up; each launch prints its own)
-        per = {k: round(d[k] / samples, 3) for k in NAMES + list(EXTRA.values())}
-        out = {"scene": scene, "config": config, "build_id": build_id, "treelet": os.environ.get("RT_DEBUG_TREELET", "0"),
+        per = {k: round(d[k] / samples, 3) for k in NAMES}
+        out = {"scene": scene, "config": config, "build_id": build_id,
                "spp_per_launch": spp, "samples": samples, "per_sample": per,
                "vmem_loads_per_sample": round(sum(d[k] for k in LOADS) / samples, 2)}
         if g.get("pairs"):
