@@ -523,7 +523,7 @@ def device_identity(rank, local):
     p = torch.cuda.get_device_properties(local)
     return {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": local,
             "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0",
-            "uuid": str(getattr(p, "uuid", "")), "name": p.name,
+            "uuid": str(getattr(p, "uuid", "")), "name": p.name, "arch": getattr(p, "gcnArchName", ""),
             "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
 
 
@@ -661,6 +661,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    # a host-side group for waits that must not hold a GPU: an RCCL barrier keeps a collective
+    # kernel spinning on every waiting rank's GPU (rank 0's C-ABI leg below uses those GPUs)
+    cpu_pg = dist.new_group(backend="gloo") if dist is not None and args.dist_backend == "nccl" else None
 
     from rt_amd import abi, render
 
@@ -778,14 +781,15 @@ def main():
     if world > 1 and not args.no_frame_abi:
         # the same strong split through the C ABI (rt_frame_*): rank 0 alone, one context on each
         # rank's device, while the other ranks wait at a barrier
-        dist.barrier()
+        torch.cuda.synchronize()
+        dist.barrier(group=cpu_pg)
         if rank == 0:
             try:
                 res["frame_abi"] = frame_abi_run(loaded, [i["device"] for i in idents], spp, args.steps,
                                                  args.warmup, digest=args.frame_digest)
             except Exception as e:  # reported, never fatal to the torch-rank headline
                 res["frame_abi"] = {"error": repr(e)[:300]}
-        dist.barrier()
+        dist.barrier(group=cpu_pg)
 
     build_id = abi.kernel_build_id()
     if rank == 0 and not args.no_roofline:
