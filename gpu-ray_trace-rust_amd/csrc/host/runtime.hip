@@ -656,6 +656,17 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
             up2 += cam->up[a] * cam->up[a];
         }
         ok = ok && (!cam->has_lens || std::fabs(cam->lens_r) * (std::sqrt(up2) + 2.0f) < lim);
+        // in_return_leaf also stands in for the root slab test: every sphere's box
+        // [fl(c - r), fl(c + r)] must lie inside the tree's bounds (true for rt_kd_build's trees),
+        // and r >= 0 orders its faces
+        for (uint32_t i = 0; i < scene->n_spheres && ok; ++i) {
+            const rt_sphere& sp = scene->spheres[i];
+            ok = sp.r >= 0.0f;
+            for (int a = 0; a < 3; ++a) {
+                const float lo = sp.c[a] - sp.r, hi = sp.c[a] + sp.r;
+                ok = ok && tree->bounds[2 * a] <= lo && hi <= tree->bounds[2 * a + 1];
+            }
+        }
         d.small_ok = ok ? 1u : 0u;
     }
     d.n_spheres = scene->n_spheres;

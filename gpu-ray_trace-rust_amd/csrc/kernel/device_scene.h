@@ -72,7 +72,7 @@ struct DevScene {
     uint32_t spheres_only;  // no free / mesh triangles: launch the sphere-only kernel
     uint32_t fastdiv;       // every split is 0 or in [2^-70, 2^61): Markstein division allowed
     uint32_t count_device;  // instrumented launch counts the device path (not the reference's)
-    uint32_t small_ok;      // sphere centres +- radii and camera below 2^58: closest_small's roots stay finite
+    uint32_t small_ok;      // closest_small allowed: coordinates below 2^58 (finite roots), r >= 0, sphere boxes inside bounds
     uint32_t restart;       // queue kernels: 0 stack, 1 stackless (kd-restart with push-down)
     uint32_t packet;        // general queue kernel: camera rays may be traced as packets (closest_packet)
     float bounds[6];

@@ -43,7 +43,7 @@ namespace rtd {
 constexpr int RT_REGEN_MIN = 12;  // sphere-only queue kernel: start new paths once this many lanes are idle or none is busy (walled +1.4%; 6: 0, 16: +1.2%)
 constexpr int RT_REGEN_MIN_BATCH = 1;  // the sphere-only kernel with batched starts (RT_START_BATCH): a start costs a few LDS reads, so idle lanes start at once (walled +6.5%; 4: +4.8%, 8: +3.5%); lens cameras, which keep per-lane starts, use it too
 constexpr int RT_REGEN_MIN_GEN = 16;  // the same for the general queue kernel: camera rays start in batches that form packets (closest_packet; a380 +2.6%)
-constexpr int RT_MIN_WAVES = 7;  // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs, no spill (measured best)
+constexpr int RT_MIN_WAVES = 7;  // __launch_bounds__ min waves per SIMD: 7 -> <=72 VGPRs (measured best; 6: -3%, 8: -2.3%)
 constexpr int RT_MIN_WAVES_GEN = 8;  // general (triangle / mesh) kernels: 8 -> <=64 VGPRs; latency-bound, +2..7% over 7 (spills outside the pass loop)
 constexpr int RT_OWNER_LOOP = 8;  // cooperative pass: owners of a pass found by a readlane loop when at most this many leaves end in it (0: binary search)
 constexpr int RT_PAIR_FETCH = 1;  // cooperative descent: a node's two children loaded together, before its decision (a380 +3%, biplane +3%)
@@ -196,15 +196,19 @@ struct Ctr {
 // {c, fl(r * r)} and its material (the host launches that kernel only when they all fit).
 // The LDS copies are file-scope __shared__ arrays referenced directly, so loads from them are
 // ds_read (a pointer that may be LDS or global would become a slower FLAT load).
-__shared__ float4 g_lds_sph[LDS_SPHERES];
 __shared__ float4 g_lds_csq[LDS_SPHERES];  // {c, fl(r * r)}: sphere.rs:92's r*r, computed once
+__shared__ float4 g_lds_lo[LDS_SPHERES];   // {fl(c - r), r}: the box's low faces (sphere.rs:106-114)
+__shared__ float4 g_lds_hi[LDS_SPHERES];   // {fl(c + r), 0}: its high faces
 __shared__ DevMat g_lds_mat[LDS_SPHERES];
 __device__ __forceinline__ uint2 fetch_node(const DevScene& sc, uint32_t i) { return sc.nodes[i]; }
 // GEN == false (sphere-only kernel): spheres come from LDS.  The general kernel reads them from
 // global memory.
 template <bool GEN>
 __device__ __forceinline__ float4 fetch_sphere(const DevScene& sc, uint32_t i) {
-    if (!GEN) return g_lds_sph[i];
+    if (!GEN) {
+        const float4 q = g_lds_csq[i];
+        return make_float4(q.x, q.y, q.z, g_lds_lo[i].w);
+    }
     return sc.sph[i];
 }
 
@@ -212,8 +216,9 @@ __device__ __forceinline__ void fill_lds_spheres(const DevScene& sc) {
     const uint32_t n = sc.n_spheres < (uint32_t)LDS_SPHERES ? sc.n_spheres : (uint32_t)LDS_SPHERES;
     for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
         const float4 v = sc.sph[i];
-        g_lds_sph[i] = v;
         g_lds_csq[i] = make_float4(v.x, v.y, v.z, v.w * v.w);
+        g_lds_lo[i] = make_float4(v.x - v.w, v.y - v.w, v.z - v.w, v.w);
+        g_lds_hi[i] = make_float4(v.x + v.w, v.y + v.w, v.z + v.w, 0.f);
         g_lds_mat[i] = sc.sph_mat[i];
     }
 }
@@ -552,28 +557,46 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, c
 // equal to the division (face - o in mk range); otherwise the traversal runs.
 //
 // The face distances are only compared, so the quotients need not be computed exactly: with
-// rc = RN(1 / d), q = RN(n * rc) lies within 2^-22 |q| of n / d (two roundings and rc's), so the
-// traversal's RN(n / d) lies in [q - |q| 2^-21, q + |q| 2^-21], and the test takes the bound on the
-// unfavourable side: t(near) <= E from q + |q| 2^-21 <= E, t(far) > L* from q - |q| 2^-21 > L*.
-// A true result is therefore true for the exact quotients; a marginal case just falls back to the
-// traversal.  (|n| < 2^61 and |rc| <= 1 / EPS: no overflow.  A product that underflows has
-// |q| < 2^-100 and an exact quotient as tiny: both are below E's floor ~1.7e-3 and L* >= HIT_MIN,
-// so the comparisons agree.  A NaN fails both compares, as before.)  This replaces the Markstein
-// quotients and their range guards: 2 x (3 + 4) instructions per axis -> 2 x 2.
-__device__ __forceinline__ bool in_return_leaf(float4 s, const Ray& r, const RayAx& ax, float e, float ls) {
-    bool ok = true;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float c = a == 0 ? s.x : (a == 1 ? s.y : s.z);
-        const float o = a == 0 ? r.o.x : (a == 1 ? r.o.y : r.o.z);
-        const float d = a == 0 ? ax.dx : (a == 1 ? ax.dy : ax.dz);
-        const float rc = a == 0 ? ax.rx : (a == 1 ? ax.ry : ax.rz);
-        const float nlo = (c - s.w) - o, nhi = (c + s.w) - o;
-        const float qlo = nlo * rc, qhi = nhi * rc;
-        const float qn = d > 0.0f ? qlo : qhi, qf = d > 0.0f ? qhi : qlo;
-        ok &= (fmaf(fabsf(qn), 0x1p-21f, qn) <= e) && (fmaf(-fabsf(qf), 0x1p-21f, qf) > ls);
-    }
-    return ok;
+// y = v_rcp_f32(d) (within 2 ulp of 1 / d; d clamped, |d| >= EPS) and q = RN(n * y), q lies within
+// 2.5 * 2^-23 |q| of n / d, and the traversal's RN(n / d) within 3 * 2^-23 |q| < 2^-21 |q| of q.
+// The bound is folded into the two thresholds once per ray: t(near) <= E follows from
+// q <= E' <= E / (1 + 2^-21) (q <= 0 gives t <= 0 < E), and t(far) > L* from q > L' =
+// RN(L* + L* 2^-20) >= L* / (1 - 2^-21).  E' = RN(L* (1 - 2^-17) - 2 EPS (1 + 2^-20)), one fma
+// below E = RN(RN(L* - 2 EPS) - RN(L* 2^-18)) by more than the 2^-21 margin for every L* >=
+// HIT_MIN (its coefficients undercut E's by 2^-18 L* and 2^-20 2 EPS, which exceed the roundings;
+// also checked on 2.2 M values).  A true result is therefore true for the exact quotients; a
+// marginal case just falls back to the traversal.  (|n| < 2^59 (small_ok) and |y| <= 1 / EPS: no
+// overflow.  A product that underflows has |q| < 2^-100 and an exact quotient as tiny: both are
+// below E's floor ~1.7e-3 and L* >= HIT_MIN, so the comparisons agree.  Only a ray with a hit
+// gets here, so o and d are finite: dot(d, o - c) involves every component.)
+//
+// With r >= 0 (small_ok) the near face's quotient is the smaller of the two faces' on every axis
+// and the far face's the larger (RN is monotone in the face and the sign of y orders them), so
+// the test is min over axes of the far quotients > L' and max over axes of the near ones <= E'.
+//
+// The root slab test (aabb.rs:22-62) needs no arithmetic of its own when this holds: the scene
+// box contains S's box (runtime.hip checks it for small_ok), so on every axis the box's far face
+// is at least as far along the ray as S's and its near face at most as far (RN is monotone in
+// the face), and the slab's products RN(RN(face - o) * RN(1 / d)) lie within 2^-23 of the exact
+// quotients.  With the bounds above, every far product exceeds L* and every near one is below
+// E < L*: entry <= L* <= exit, the slab test passes and fl(exit + EPS) >= L*, which is what the
+// shortcut needs.  Lanes that fail it compute the exact slab and take the traversal.
+// lo / hi: S's box faces fl(c -+ r) (g_lds_lo / g_lds_hi).
+__device__ __forceinline__ bool in_return_leaf(float4 lo, float4 hi, const Ray& r, float ls) {
+    const float en = fmaf(ls, 1.0f - 0x1p-17f, -2.0f * EPS * (1.0f + 0x1p-20f));  // E'
+    const float lf = fmaf(ls, 0x1p-20f, ls);                                      // L'
+    // the EPS-clamped direction of the traversal (kdtree.rs:75-77): d itself unless some lane of
+    // the wave has a component below EPS (~2% of a wave's segments)
+    V3 dc = r.d;
+    if (__builtin_expect(__ballot(fminf(fminf(fabsf(dc.x), fabsf(dc.y)), fabsf(dc.z)) < EPS) != 0, 0))
+        dc = mk(clamp_eps(dc.x), clamp_eps(dc.y), clamp_eps(dc.z));
+    const float yx = __builtin_amdgcn_rcpf(dc.x), yy = __builtin_amdgcn_rcpf(dc.y), yz = __builtin_amdgcn_rcpf(dc.z);
+    const float lx = (lo.x - r.o.x) * yx, hx = (hi.x - r.o.x) * yx;
+    const float ly = (lo.y - r.o.y) * yy, hy = (hi.y - r.o.y) * yy;
+    const float lz = (lo.z - r.o.z) * yz, hz = (hi.z - r.o.z) * yz;
+    const float vp = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fminf(lz, hz));
+    const float wp = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fmaxf(lz, hz));
+    return vp <= en && wp > lf;
 }
 
 // KdTree::closest_ray_hit (kdtree.rs:58-64): root slab test, stack search, then the
@@ -622,28 +645,30 @@ __device__ __forceinline__ bool closest_small(const DevScene& sc, const Ray& r, 
         const float4 sa = g_lds_csq[i];
         take(sphere_disc(sa, sa.w, r), i);
     }
-    float root_entry, root_exit;
-    const RayAx ax = ray_axes(r);
-    if (any && entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
+    if (any) {
         RC(RC_SLAB);
-        // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
-        const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
         // (COUNT here means the device-work count: closest_small never runs for the reference's)
-        if (root_entry <= ls && ls <= root_exit + EPS && in_return_leaf(fetch_sphere<false>(sc, imin), r, ax, e, ls)) {
+        if (in_return_leaf(g_lds_lo[imin], g_lds_hi[imin], r, ls)) {
             best->ref = (K_SPHERE << REF_KIND_SHIFT) | imin;
             best->l = ls;
             best->bu = best->bv = 0.f;
             return true;
         }
-        const float entry = fmaxf(root_entry, e);
         RC(RC_FALLBACK);
-        bool found;
-        const bool fast = sc.fastdiv && origin_fast_ok(r.o);
-        if (__builtin_expect(__ballot(!fast) == 0, 1))
-            found = stack_search<COUNT, false, true, true, RESTART>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
-        else
-            found = stack_search<COUNT, false, false, true, RESTART>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
-        if (found) return true;
+        float root_entry, root_exit;
+        const RayAx ax = ray_axes(r);
+        if (entry_exit(sc.bounds, ax, r, &root_entry, &root_exit)) {
+            // fl(x + EPS) < L* for all x <= E: margin 2 EPS + 2^-18 L* (>> rounding of L*)
+            const float e = (ls - 2.0f * EPS) - ls * 0x1p-18f;
+            const float entry = fmaxf(root_entry, e);
+            bool found;
+            const bool fast = sc.fastdiv && origin_fast_ok(r.o);
+            if (__builtin_expect(__ballot(!fast) == 0, 1))
+                found = stack_search<COUNT, false, true, true, RESTART>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
+            else
+                found = stack_search<COUNT, false, false, true, RESTART>(sc, r, ax, entry, root_exit, best, st, c, imin, ls);
+            if (found) return true;
+        }
     }
     if (sc.has_cube) {
         best->ref = REF_CUBE;

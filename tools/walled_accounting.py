@@ -121,8 +121,10 @@ def event_of(stack, L):
             if has("leaf_closest"):
                 return "fb_leaves"
             return "fb_nodes" if (has("split_t") or has("fetch_node") or has("sel3")) else "fallback"
-        if has("in_return_leaf") or has("entry_exit") or has("fetch_sphere"):
+        if has("in_return_leaf") or has("fetch_sphere"):
             return "slab"
+        if has("entry_exit") or has("ray_axes"):
+            return "fallback"  # round 6: the exact slab runs only where the shortcut failed
         # the sphere loop: pairs (lines pair0..pair1: two copies, 6 iterations for 13 spheres) and
         # the remainder (one copy, one iteration); a copy's share of the root computations is
         # taken as its share of the spheres (6/13 per pair copy, 1/13 for the remainder)
@@ -138,6 +140,8 @@ def event_of(stack, L):
         ln = lines.get("closest_small", 0)
         if L["slab0"] <= ln <= L["slab1"]:
             return "slab"
+        if L["slab1"] < ln <= L["fb1"]:
+            return "fallback"
         return "iter"
     if has("closest"):
         return "dead"  # the general (non-small) traversal: walled always takes closest_small
@@ -182,12 +186,13 @@ def anchors():
     L = {"ballot": src_line("__ballot(q.thing2 > 0.0f) == 0"),
          "pair0": src_line("const SphDisc qa = sphere_disc(sa, sa.w, r)") - 2,
          "pair1": src_line("const SphDisc qa = sphere_disc(sa, sa.w, r)") + 3,
-         "slab0": src_line("RC(RC_SLAB)") - 1, "slab1": src_line("RC(RC_FALLBACK)") + 8,
+         "slab0": src_line("RC(RC_SLAB)") - 1, "slab1": src_line("RC(RC_FALLBACK)") - 1,
          "seed": src_line("seed_diff = draw(&p.rng) < m->diffp"),
          "rr0": src_line("russian_roulette_filter"), "rr1": src_line("russian_roulette_filter") + 5,
          "spec0": src_line("RC(RC_SPEC)") - 1, "spec1": src_line("RC(RC_SPEC)") + 1,
          "regen0": src_line("RC(RC_REGEN)") - 1, "batch0": src_line("RC(RC_BATCH)") - 1,
          "loop": src_line("const uint64_t need = __ballot(!have && !done)")}
+    L["fb1"] = src_line("if (found) return true;", L["slab1"])
     L["batch1"] = src_line("st_n = 64u - st_pos;", L["batch0"])
     L["dead0"] = src_line("} else if (regen) {", L["regen0"])
     L["regen1"] = L["dead0"] - 1
@@ -201,7 +206,7 @@ def table(path, sq_valu):
     d = json.load(open(path))
     n = d["counts"]
     elf = os.path.join(PKG, "build", "trace_lines.elf")
-    bl, R = blocks(elf, "queue_kernelILb0ELb0ELb1ELb0E")
+    bl, R = blocks(elf, "queue_kernelILb0ELb0ELb1EE")
     L = anchors()
     # the launch's waves: the grid is the resident workgroups (2 waves each), ~7 per SIMD
     waves = n.get("waves") or d.get("grid_waves") or 256 * 4 * 7
