@@ -43,9 +43,10 @@ OPS = {
     # running minimum (sqrt, -dir, two adds, l1 > 0, select, l >= HIT_MIN, l < best, two
     # selects); the closest hit needs every such sphere's length
     "sphere_roots": 10,
-    # per segment that hits: ray_axes (3 clamps of 3, 3 reciprocals) 12; the root slab test 22;
-    # in_return_leaf (3 axes x 10, the descent floor 3) 33
-    "hit_segment": 12 + 22 + 33,
+    # per segment that hits: in_return_leaf (round 6: it stands in for the root slab test) — the
+    # two thresholds 2, per axis a reciprocal, two face differences and two products 15, near and
+    # far per axis and their max / min over the axes 10, two compares 2
+    "hit_segment": 2 + 15 + 10 + 2,
     # per sphere hit: hit_info (perfect 6, normalize(perfect - c) 12, pos 6), emission 6, T *= rgb
     # * p 6, d.n 5, the mirror direction 9
     "hit": 24 + 6 + 6 + 5 + 9,
