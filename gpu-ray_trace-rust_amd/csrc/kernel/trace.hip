@@ -1814,7 +1814,10 @@ __device__ __forceinline__ void make_start(const LaunchArgs& a, const DevScene& 
     e[5][lane] = slot;
 }
 
-template <bool GEN, bool DLS, bool RESTART>
+// STARTS (sphere-only kernel): paths start per lane (a lens camera, or no pixel table), not in the
+// LDS batches.  A template parameter rather than a runtime flag: with both start paths in one
+// loop, their merged Path state cost walled ~15 register copies per segment (+0.7% without).
+template <bool GEN, bool DLS, bool RESTART, bool STARTS = false>
 __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void queue_kernel(
     LaunchArgs a, const uint2* __restrict__ pk_nodes, const uint32_t* __restrict__ pk_refs,
     const float4* __restrict__ pk_prim4) {
@@ -1832,7 +1835,7 @@ __global__ __launch_bounds__(BLOCK, GEN ? RT_MIN_WAVES_GEN : RT_MIN_WAVES) void 
     const uint32_t lane = __lane_id();
     uint32_t pool = 0, pool_end = 0;  // wave-uniform: unclaimed items [pool, pool_end)
     const uint32_t n_waves = gridDim.x * (TPB / 64);
-    const bool batch_ok = !GEN && !sc.has_lens && a.pix_q != nullptr;
+    constexpr bool batch_ok = !GEN && !STARTS;  // the host launches it so: no lens, a pixel table
     const uint32_t shard_waves = (n_waves + a.n_shards - 1) / a.n_shards;
     // (the batch starts use one counter over all the items: the first grab is sized for that)
     uint32_t grab = batch_ok ? grab_size<GEN>(a.n_items, n_waves) : grab_size<GEN>(a.n_items / a.n_shards, shard_waves);
@@ -2060,7 +2063,11 @@ hipError_t launch_trace(const LaunchArgs& a, hipStream_t s) {
 template <class F>
 static hipError_t with_queue_kernel(const LaunchArgs& a, F f) {
     const bool rs = a.sc.restart != 0;
-    if (a.sc.spheres_only) return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
+    if (a.sc.spheres_only) {
+        if (a.sc.has_lens || a.pix_q == nullptr)  // per-lane path starts
+            return rs ? f(queue_kernel<false, false, true, true>, false) : f(queue_kernel<false, false, false, true>, false);
+        return rs ? f(queue_kernel<false, false, true>, false) : f(queue_kernel<false, false, false>, false);
+    }
     if (a.sc.dls) return rs ? f(queue_kernel<true, true, true>, true) : f(queue_kernel<true, true, false>, true);
     return rs ? f(queue_kernel<true, false, true>, true) : f(queue_kernel<true, false, false>, true);
 }

@@ -53,9 +53,10 @@ def test_every_kernel_has_a_body():
 
     sizes = _kernel_sizes(_gfx950_object(abi.LIB_PATH))
     queue = {k: v for k, v in sizes.items() if "queue_kernel" in k}
-    # queue_kernel<GEN, DLS, RESTART>: sphere-only, general and DLS, each with the stack and the
-    # stackless traversal (round 6: the measured-slower LDS slab and pool kernels are gone)
-    assert len(queue) == 6, sorted(queue)
+    # queue_kernel<GEN, DLS, RESTART, STARTS>: general and DLS, each with the stack and the
+    # stackless traversal; sphere-only the same, each with batched and per-lane path starts
+    # (round 6: the measured-slower LDS slab and pool kernels are gone)
+    assert len(queue) == 8, sorted(queue)
     for name, size in sorted(sizes.items()):
         if "kernel" in name:
             assert size > 256, f"{name}: {size} B of code (an empty kernel is 4)"

@@ -137,3 +137,23 @@ def test_empty_leaves_with_stale_offsets(gpu_available, monkeypatch):
     with render.Context(sc) as c:
         full = c.render(None, 0, 2)
     assert not np.array_equal(full, ref)
+
+
+def test_shortcut_needs_bounds_around_every_sphere(gpu_available):
+    """closest_small's in_return_leaf stands in for the root slab test only when the tree's bounds
+    contain every sphere's box (runtime.hip small_ok).  With the builder's tree the
+    shortcut runs (a few node visits per sample against the reference's hundreds); a caller tree
+    whose bounds cut the +x wall sphere's box must take the plain traversal, which does at least
+    the reference's node work (the kd-restart only adds visits)."""
+    from rt_amd import render
+    from conftest import load_scene
+
+    sc = load_scene("walled", width=80, height=40)
+    tree = render.KdTree(sc.desc, int(sc.info.kd_tree_depth))
+    with render.Context(sc, tree=tree.as_struct()) as c:
+        dev, ref = c.count_work(None, 0, 2, device=True), c.count_work(None, 0, 2)
+    assert dev["segments"] == ref["segments"] and dev["nodes"] < 0.01 * ref["nodes"], (dev, ref)
+    tree.bounds[1] = tree.bounds[1] * 0.5  # x max: 1015 -> 507, inside the wall sphere's [15, 1015]
+    with render.Context(sc, tree=tree.as_struct()) as c:
+        dev_cut, ref_cut = c.count_work(None, 0, 2, device=True), c.count_work(None, 0, 2)
+    assert dev_cut["nodes"] >= ref_cut["nodes"] > 0.5 * ref["nodes"], (dev_cut, ref_cut)

@@ -8,7 +8,7 @@ path starts, queue, ...).  Prints, per region, the instruction counts by class (
 SMEM, LDS, branch/wait), and — with --samples, a CSV of PC samples (address, count) from
 rocprofv3 --pc-sampling — the sampled share of each region.
 
-Usage: python tools/isa_regions.py [--kernel 'queue_kernelILb0ELb0ELb1EE'] [--samples pcs.csv] [--json out]
+Usage: python tools/isa_regions.py [--kernel 'queue_kernelILb0ELb0ELb1ELb0EE'] [--samples pcs.csv] [--json out]
 """
 import argparse
 import collections
@@ -98,7 +98,7 @@ def klass(mn):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="queue_kernelILb0ELb0ELb1EE")
+    ap.add_argument("--kernel", default="queue_kernelILb0ELb0ELb1ELb0EE")
     ap.add_argument("--lines-elf", default=os.path.join(PKG, "build", "trace_lines.elf"))
     ap.add_argument("--lib", default=os.path.join(PKG, "lib", "librt_amd.so"))
     ap.add_argument("--samples", default=None, help="CSV of pc,count (absolute code-object addresses)")

@@ -206,7 +206,7 @@ def table(path, sq_valu):
     d = json.load(open(path))
     n = d["counts"]
     elf = os.path.join(PKG, "build", "trace_lines.elf")
-    bl, R = blocks(elf, "queue_kernelILb0ELb0ELb1EE")
+    bl, R = blocks(elf, "queue_kernelILb0ELb0ELb1ELb0EE")
     L = anchors()
     # the launch's waves: the grid is the resident workgroups (2 waves each), ~7 per SIMD
     waves = n.get("waves") or d.get("grid_waves") or 256 * 4 * 7
