@@ -661,7 +661,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         // and r >= 0 orders its faces
         for (uint32_t i = 0; i < scene->n_spheres && ok; ++i) {
             const rt_sphere& sp = scene->spheres[i];
-            ok = sp.r >= 0.0f;
+            ok = ok && sp.r >= 0.0f;
             for (int a = 0; a < 3; ++a) {
                 const float lo = sp.c[a] - sp.r, hi = sp.c[a] + sp.r;
                 ok = ok && tree->bounds[2 * a] <= lo && hi <= tree->bounds[2 * a + 1];

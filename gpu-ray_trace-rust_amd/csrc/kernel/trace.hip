@@ -564,7 +564,7 @@ __device__ __forceinline__ bool stack_search(const DevScene& sc, const Ray& r, c
 // RN(L* + L* 2^-20) >= L* / (1 - 2^-21).  E' = RN(L* (1 - 2^-17) - 2 EPS (1 + 2^-20)), one fma
 // below E = RN(RN(L* - 2 EPS) - RN(L* 2^-18)) by more than the 2^-21 margin for every L* >=
 // HIT_MIN (its coefficients undercut E's by 2^-18 L* and 2^-20 2 EPS, which exceed the roundings;
-// also checked on 2.2 M values).  A true result is therefore true for the exact quotients; a
+// tests/test_small_bound.py).  A true result is therefore true for the exact quotients; a
 // marginal case just falls back to the traversal.  (|n| < 2^59 (small_ok) and |y| <= 1 / EPS: no
 // overflow.  A product that underflows has |q| < 2^-100 and an exact quotient as tiny: both are
 // below E's floor ~1.7e-3 and L* >= HIT_MIN, so the comparisons agree.  Only a ray with a hit
