@@ -659,6 +659,7 @@ static int create_impl(rt_ctx* c, const rt_scene_desc* scene, const rt_camera* c
         // in_return_leaf also stands in for the root slab test: every sphere's box
         // [fl(c - r), fl(c + r)] must lie inside the tree's bounds (true for rt_kd_build's trees),
         // and r >= 0 orders its faces
+        ok = ok && tree->n_nodes > 0;
         for (uint32_t i = 0; i < scene->n_spheres && ok; ++i) {
             const rt_sphere& sp = scene->spheres[i];
             ok = ok && sp.r >= 0.0f;
