@@ -595,8 +595,8 @@ def frame_abi_run(loaded, devices, spp, steps, warmup, digest=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="walled")
     ap.add_argument("--spp-per-step", type=int, default=None,
                     help="samples per pixel per step (default: the scheme's gpu_render_batch)")
